@@ -1,0 +1,77 @@
+"""Synthetic U-RED batches and source-part database (numpy, PCG64-seeded).
+
+The reference ships no data and reads absolute /mnt/d paths plus per-part
+pickles inside every step (engine/global_variables.py:13-37,
+dataset/dataset_utils.py:1101-1143). Benchmarks and parity tests therefore use
+this generator, which produces exactly the arrays the reference's train loop
+holds after get_labels / get_source_info / get_source_points
+(engine/train.py:196-210), following SURVEY.md §8(d):
+
+  target cloud x[b]   N points uniform in the unit ball, normalize_pts'ed
+                      (engine/geometry_utils.py:88-94)
+  part labels         k_b parts as y-quantile slabs, labels 0..k_b-1
+  semantics           per part uniform in [0, 42) (the label_to_idx range)
+  source DB           per part 1024 points uniform in a random AABB; points_mat
+                      A = [I3 | diag(q)], q = (p - c)/s (engine/run_preprocessing.py:118-165
+                      with R = I); default_param = [c, s]
+  pseudo-labels       a source index per valid part slot, -1 for padding; -1
+                      resolves to the last source (Python negative indexing,
+                      dataset/dataset_utils.py:800-805)
+"""
+import numpy as np
+
+NUM_SEM = 42
+NP_PER_PART = 1024
+
+
+def normalize_pts(p):
+    out = np.asarray(p, np.float32).copy()
+    out -= out.mean(axis=0)
+    out /= np.sqrt(np.max(np.sum(out ** 2, axis=1)))
+    return out
+
+
+def make_source_db(num_sources, seed=1, np_per_part=NP_PER_PART):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    c = rng.uniform(-0.5, 0.5, size=(num_sources, 3)).astype(np.float32)
+    s = rng.uniform(0.05, 0.5, size=(num_sources, 3)).astype(np.float32)
+    q = rng.uniform(-1.0, 1.0, size=(num_sources, np_per_part, 3)).astype(np.float32)
+    pts = (c[:, None, :] + q * s[:, None, :]).astype(np.float32)
+    # A per point: rows (x,y,z), cols [t_x t_y t_z s_x s_y s_z]: p = t + diag(q) s
+    A = np.zeros((num_sources, np_per_part, 3, 6), np.float32)
+    for r in range(3):
+        A[:, :, r, r] = 1.0
+        A[:, :, r, 3 + r] = q[:, :, r]
+    mats = A.reshape(num_sources, np_per_part * 3, 6)
+    default_param = np.concatenate([c, s], axis=1).astype(np.float32)
+    sem = rng.integers(0, NUM_SEM, size=num_sources).astype(np.int64)
+    return {"src_points": pts, "src_mats": mats, "src_default_param": default_param, "src_sem": sem}
+
+
+def make_batch(batch_size, num_points, num_sources, max_parts=16, parts=4, seed=0, invalid_frac=0.0):
+    """One synthetic batch. `parts` is an int (k_b for every sample) or a list per sample."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    B, N = batch_size, num_points
+    ks = [parts] * B if np.isscalar(parts) else list(parts)
+    assert len(ks) == B and all(1 <= k <= max_parts for k in ks) and all(k <= N for k in ks)
+    x = np.zeros((B, N, 3), np.float32)
+    labels = np.zeros((B, N), np.int64)
+    tgt_sem = np.zeros((B, N), np.int64)
+    src_labels = np.full((B, max_parts), -1, np.int64)
+    for b in range(B):
+        d = rng.standard_normal((N, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        r = rng.uniform(0, 1, size=(N, 1)) ** (1.0 / 3.0)
+        x[b] = normalize_pts(d * r)
+        rank = np.empty(N, np.int64)
+        rank[np.argsort(x[b, :, 1], kind="stable")] = np.arange(N)
+        labels[b] = (rank * ks[b]) // N
+        psem = rng.integers(0, NUM_SEM, size=ks[b])
+        tgt_sem[b] = psem[labels[b]]
+        src = rng.integers(0, num_sources, size=ks[b])
+        if invalid_frac > 0:
+            src[rng.uniform(size=ks[b]) < invalid_frac] = -1
+        src_labels[b, :ks[b]] = src
+    src_index = np.where(src_labels < 0, num_sources - 1, src_labels)
+    return {"x": x, "labels": labels, "tgt_sem": tgt_sem, "src_labels": src_labels,
+            "src_index": src_index, "parts": np.asarray(ks, np.int64)}

@@ -1,0 +1,93 @@
+"""ctypes loader for libured_hip.so (the C-ABI declared in include/ured_hip.h).
+
+There is no CPU fallback: if the library is missing, or a tensor is not on a
+ROCm device, the call raises. torch is imported *before* the library is
+dlopen'ed so that the library's libamdhip64.so.7 dependency binds to the HIP
+runtime torch already loaded (one runtime per process).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libured_hip.so"
+LIB_PATH = os.path.join(_HERE, LIB_NAME)
+ABI_VERSION = 1
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+
+# name -> argtypes (all functions return int status, 0 = ok)
+_SIGNATURES = {
+    "ured_nn_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "ured_nn_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "ured_nn_seg_fwd": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "ured_nn_seg_bwd": [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+}
+
+_lib = None
+
+
+class UredError(RuntimeError):
+    """A libured_hip.so entry point returned a non-zero status."""
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises ImportError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is not built. Build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` from the repo root.")
+    handle = ctypes.CDLL(LIB_PATH)
+    handle.ured_abi_version.restype = ctypes.c_int
+    handle.ured_abi_version.argtypes = []
+    handle.ured_last_error.restype = ctypes.c_char_p
+    handle.ured_last_error.argtypes = []
+    got = handle.ured_abi_version()
+    if got != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI version {got}, expected {ABI_VERSION}")
+    for name, argtypes in _SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    _lib = handle
+    return _lib
+
+
+def exported_symbols():
+    return ["ured_abi_version", "ured_last_error"] + list(_SIGNATURES)
+
+
+def call(name, *args):
+    """Call entry point `name`; raise UredError with the library's message on failure."""
+    handle = lib()
+    rc = getattr(handle, name)(*args)
+    if rc != 0:
+        msg = handle.ured_last_error().decode(errors="replace")
+        raise UredError(f"{name} failed (status {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    """The current torch stream on t's device, as a hipStream_t handle."""
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                "ured_hip ops run on the MI355X only (GPU tensors only, like the reference "
+                "chamfer3D extension); got a tensor on " + str(t.device))

@@ -1,0 +1,126 @@
+"""Nearest-neighbour (chamfer) ops on libured_hip.so, as torch autograd Functions.
+
+Dense form  : drop-in for chamfer_3DFunction
+              (Density_aware_Chamfer_Distance/utils_v2/metrics/CD/chamfer3D/dist_chamfer_3D.py:26-64).
+Ragged form : one launch for a whole family of per-sample / per-part chamfer
+              calls (loss/chamfer_loss.py:13-30, loss/basic_loss.py:249-265).
+Distances are squared L2 (fp32); indices int32, lowest index on ties.
+"""
+import torch
+from torch.autograd import Function
+
+from . import _lib
+
+
+def _as_points(t, name):
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32 points, got {t.dtype}")
+    if t.shape[-1] != 3:
+        raise ValueError(f"{name}: last dim must be 3, got shape {tuple(t.shape)}")
+    return t.contiguous()
+
+
+class NNDenseFunction(Function):
+    """(xyz1 [b,n,3], xyz2 [b,m,3]) -> (dist1 [b,n], dist2 [b,m], idx1 [b,n] i32, idx2 [b,m] i32)."""
+
+    @staticmethod
+    def forward(ctx, xyz1, xyz2):
+        xyz1 = _as_points(xyz1, "xyz1")
+        xyz2 = _as_points(xyz2, "xyz2")
+        _lib.require_device(xyz1, xyz2)
+        if xyz1.dim() != 3 or xyz2.dim() != 3 or xyz1.shape[0] != xyz2.shape[0]:
+            raise ValueError(f"expected [b,n,3] and [b,m,3], got {tuple(xyz1.shape)} {tuple(xyz2.shape)}")
+        b, n, _ = xyz1.shape
+        m = xyz2.shape[1]
+        dev = xyz1.device
+        dist1 = torch.empty(b, n, device=dev, dtype=torch.float32)
+        dist2 = torch.empty(b, m, device=dev, dtype=torch.float32)
+        idx1 = torch.empty(b, n, device=dev, dtype=torch.int32)
+        idx2 = torch.empty(b, m, device=dev, dtype=torch.int32)
+        if n == 0 or m == 0:
+            dist1.zero_(); dist2.zero_(); idx1.zero_(); idx2.zero_()
+        else:
+            _lib.call("ured_nn_fwd", _lib.ptr(xyz1), _lib.ptr(xyz2), b, n, m, 3,
+                      _lib.ptr(dist1), _lib.ptr(idx1), _lib.ptr(dist2), _lib.ptr(idx2),
+                      _lib.stream_of(xyz1))
+        ctx.save_for_backward(xyz1, xyz2, idx1, idx2)
+        ctx.mark_non_differentiable(idx1, idx2)
+        return dist1, dist2, idx1, idx2
+
+    @staticmethod
+    def backward(ctx, gd1, gd2, _gi1, _gi2):
+        xyz1, xyz2, idx1, idx2 = ctx.saved_tensors
+        b, n, _ = xyz1.shape
+        m = xyz2.shape[1]
+        g1 = torch.zeros_like(xyz1)
+        g2 = torch.zeros_like(xyz2)
+        if n and m and (gd1 is not None or gd2 is not None):
+            gd1 = gd1.contiguous() if gd1 is not None else None
+            gd2 = gd2.contiguous() if gd2 is not None else None
+            _lib.call("ured_nn_bwd", _lib.ptr(xyz1), _lib.ptr(xyz2), b, n, m,
+                      _lib.ptr(gd1), _lib.ptr(gd2), _lib.ptr(idx1), _lib.ptr(idx2),
+                      _lib.ptr(g1), _lib.ptr(g2), _lib.stream_of(xyz1))
+        return g1, g2
+
+
+class NNSegFunction(Function):
+    """Ragged NN over segment pairs (see ured_nn_seg_fwd in include/ured_hip.h).
+
+    a [Na,3], b [Nb,3] flat point buffers; segs int32 [nseg,4] device table of
+    (a_off, a_len, b_off, b_len); max_a / max_b host upper bounds of the lengths.
+    Returns dist_a [Na], idx_a [Na], dist_b [Nb], idx_b [Nb]; points outside every
+    pair get dist 0 / idx 0 (and no gradient).
+    """
+
+    @staticmethod
+    def forward(ctx, a, b, segs, max_a, max_b, dirs):
+        a = _as_points(a, "a").reshape(-1, 3)
+        b = _as_points(b, "b").reshape(-1, 3)
+        _lib.require_device(a, b, segs)
+        if segs.dtype != torch.int32 or segs.dim() != 2 or segs.shape[1] != 4:
+            raise ValueError("segs must be an int32 [nseg,4] tensor")
+        segs = segs.contiguous()
+        dev = a.device
+        dist_a = torch.zeros(a.shape[0], device=dev, dtype=torch.float32)
+        idx_a = torch.zeros(a.shape[0], device=dev, dtype=torch.int32)
+        dist_b = torch.zeros(b.shape[0], device=dev, dtype=torch.float32)
+        idx_b = torch.zeros(b.shape[0], device=dev, dtype=torch.int32)
+        nseg = segs.shape[0]
+        if nseg:
+            _lib.call("ured_nn_seg_fwd", _lib.ptr(a), _lib.ptr(b), _lib.ptr(segs), nseg,
+                      int(max_a), int(max_b), int(dirs),
+                      _lib.ptr(dist_a), _lib.ptr(idx_a), _lib.ptr(dist_b), _lib.ptr(idx_b),
+                      _lib.stream_of(a))
+        ctx.save_for_backward(a, b, segs, idx_a, idx_b)
+        ctx.max_a, ctx.max_b, ctx.dirs = int(max_a), int(max_b), int(dirs)
+        ctx.mark_non_differentiable(idx_a, idx_b)
+        return dist_a, idx_a, dist_b, idx_b
+
+    @staticmethod
+    def backward(ctx, gd_a, _gia, gd_b, _gib):
+        a, b, segs, idx_a, idx_b = ctx.saved_tensors
+        ga = torch.zeros_like(a)
+        gb = torch.zeros_like(b)
+        if not (ctx.dirs & 1):
+            gd_a = None
+        if not (ctx.dirs & 2):
+            gd_b = None
+        if segs.shape[0] and (gd_a is not None or gd_b is not None):
+            gd_a = gd_a.contiguous() if gd_a is not None else None
+            gd_b = gd_b.contiguous() if gd_b is not None else None
+            _lib.call("ured_nn_seg_bwd", _lib.ptr(a), _lib.ptr(b), _lib.ptr(segs), segs.shape[0],
+                      ctx.max_a, ctx.max_b, _lib.ptr(gd_a), _lib.ptr(gd_b),
+                      _lib.ptr(idx_a), _lib.ptr(idx_b), _lib.ptr(ga), _lib.ptr(gb),
+                      _lib.stream_of(a))
+        return ga, gb, None, None, None, None
+
+
+def nn_dense(xyz1, xyz2):
+    return NNDenseFunction.apply(xyz1, xyz2)
+
+
+def nn_segments(a, b, segs, max_a, max_b, dirs=3):
+    """Returns dist_a, idx_a, dist_b, idx_b over the flat buffers (see NNSegFunction)."""
+    a_shape, b_shape = a.shape[:-1], b.shape[:-1]
+    da, ia, db, ib = NNSegFunction.apply(a, b, segs, max_a, max_b, dirs)
+    return da.view(a_shape), ia.view(a_shape), db.view(b_shape), ib.view(b_shape)

@@ -1,0 +1,436 @@
+"""CPU restatement of the U-RED training step — TEST INFRASTRUCTURE ONLY.
+
+This is the parity checker for the HIP path (and the cpu_baseline leg of
+bench.py). It is written functionally over plain state_dict-keyed parameter
+dicts, following (reference root = the U-RED repo):
+
+  TargetEncoder.forward          network/simple_encoder.py:88-107
+  re_residual_net.forward        network/deformation_net.py:96-107 (+ FeedForwardNet_norm,
+                                 attention_graph/attention_utils.py:62-86: Conv -> ReLU -> BN)
+  DeformNet_MatchingNet.forward  network/deformation_net.py:74-93
+  GraphAttentionNet & co.        attention_graph/attention_gnn.py:8-98, attention.py:8-19
+  get_part                       engine/train.py:103-136 (+ compute_aabbox dataset/dataset_utils.py:77-85)
+  get_shape / get_symmetric      dataset/dataset_utils.py:691-726, :1194-1196
+  compute_cm_loss                loss/chamfer_loss.py:5-30
+  residual_retrieval_loss        loss/basic_loss.py:249-265
+  consistency losses             loss/basic_consistency_loss.py:4-22
+  contrast loss                  loss/contrast_loss.py:61-102
+  loss assembly / optimiser      engine/train.py:196-345, train_utils/optimizer_dm.py:68-104
+
+Pinned against reference-generated golden vectors (tests/golden/make_golden.py).
+Shape_Measure.ChamferLoss is absent from the reference tree (unpinned); it is
+taken to return squared NN distances, as the in-tree chamfer_3DDist does.
+"""
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import nn_ref
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+# ----------------------------------------------------------------------------
+# architecture description -> state_dict key/shape lists (same keys as the reference)
+# ----------------------------------------------------------------------------
+
+
+def _conv(prefix, cin, cout, k=True):
+    return [(prefix + ".weight", (cout, cin, 1) if k else (cout, cin), "w", cin),
+            (prefix + ".bias", (cout,), "b", cin)]
+
+
+def _bn(prefix, c):
+    return [(prefix + ".weight", (c,), "gamma", c), (prefix + ".bias", (c,), "beta", c),
+            (prefix + ".running_mean", (c,), "rm", c), (prefix + ".running_var", (c,), "rv", c),
+            (prefix + ".num_batches_tracked", (), "nbt", c)]
+
+
+def _stn_keys(prefix, cin):
+    k = []
+    k += _conv(prefix + ".mlp1.0", cin, 64) + _bn(prefix + ".mlp1.1", 64)
+    k += _conv(prefix + ".mlp1.3", 64, 128) + _bn(prefix + ".mlp1.4", 128)
+    k += _conv(prefix + ".mlp1.6", 128, 1024) + _bn(prefix + ".mlp1.7", 1024)
+    k += _conv(prefix + ".mlp2.0", 1024, 512, False) + _bn(prefix + ".mlp2.1", 512)
+    k += _conv(prefix + ".mlp2.3", 512, 256, False) + _bn(prefix + ".mlp2.4", 256)
+    k += _conv(prefix + ".mlp2.6", 256, cin * cin, False)
+    return k
+
+
+def target_encoder_keys(emb, sem, cin=3):
+    k = _stn_keys("stn1", cin) + _stn_keys("stn2", 64)
+    k += _conv("mlp1.0", cin, 64) + _bn("mlp1.1", 64) + _conv("mlp1.3", 64, 64) + _bn("mlp1.4", 64)
+    k += _conv("mlp2.0", 64, 64) + _bn("mlp2.1", 64) + _conv("mlp2.3", 64, 128) + _bn("mlp2.4", 128)
+    k += _conv("mlp2.6", 128, 1024) + _bn("mlp2.7", 1024)
+    k += _conv("fuse_sem.0", 1024 + sem, 1024) + _bn("fuse_sem.1", 1024)
+    k += _conv("per_point_out.0", 1024, emb) + _bn("per_point_out.1", emb) + _conv("per_point_out.3", emb, emb)
+    k += _conv("fc", 1024, emb, False)
+    return k
+
+
+def ffn_norm_keys(prefix, dims, use_bn):
+    k, i = [], 0
+    for a, b in zip(dims[:-2], dims[1:-1]):
+        k += _conv(f"{prefix}.{i}", a, b)
+        if use_bn:
+            k += _bn(f"{prefix}.{i + 2}", b)
+            i += 3
+        else:
+            i += 2
+    k += _conv(f"{prefix}.{i}", dims[-2], dims[-1])
+    return k
+
+
+def residual_net_keys(cin):
+    return ffn_norm_keys("residual_net", [cin, 256, 256, 32, 3], True)
+
+
+def deform_net_keys(c, num_stages=2, part_latent_dim=256):
+    k = ffn_norm_keys("part_encoding", [part_latent_dim, 128, c], False)
+    k += ffn_norm_keys("param_decoder", [3 * c, 256, 6], False)
+    for L in range(2 * num_stages):
+        p = f"graph_attention_net.layers.{L}.module"
+        for nm in ("in_proj_q", "in_proj_k", "in_proj_v", "out_proj"):
+            k += _conv(f"{p}.mha.{nm}", c, c)
+        k += ffn_norm_keys(f"{p}.fc", [2 * c, 2 * c, c], True)
+    return k
+
+
+def model_keys(cfg):
+    C, S = cfg["source_latent_dim"], cfg["sem_latent_dim"]
+    Ct = cfg["target_latent_dim"]
+    return OrderedDict([
+        ("target_encoder_full", target_encoder_keys(Ct, S)),
+        ("param_decoder_full", deform_net_keys(C)),
+        ("re_residual_net_full", residual_net_keys(2 * Ct)),
+        ("recon_decoder_full", residual_net_keys(2 * Ct)),
+        ("src_encoder_all", target_encoder_keys(C, S)),
+        ("recon_decoder_src", residual_net_keys(2 * C)),
+        ("embedding_layer", [("weight", (42, S), "emb", S)]),
+    ])
+
+
+def make_params(cfg, seed=0, bn_jitter=0.1):
+    """Deterministic parameters for every reference state_dict key.
+
+    Weights/biases ~ U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (torch's default bound),
+    BN gamma = 1 + jitter*U(-1,1), beta = jitter*U(-1,1), running stats (0, 1),
+    embedding ~ N(0,1). Each tensor has its own PCG64 stream keyed by its name.
+    """
+    out = OrderedDict()
+    for mod, keys in model_keys(cfg).items():
+        sd = OrderedDict()
+        for name, shape, kind, fan in keys:
+            h = int.from_bytes(f"{mod}.{name}".encode(), "little") % (2 ** 63)
+            rng = np.random.Generator(np.random.PCG64([seed, h % (2 ** 32), h >> 32]))
+            if kind in ("w", "b"):
+                bound = 1.0 / math.sqrt(fan)
+                v = rng.uniform(-bound, bound, size=shape)
+            elif kind == "gamma":
+                v = 1.0 + bn_jitter * rng.uniform(-1, 1, size=shape)
+            elif kind == "beta":
+                v = bn_jitter * rng.uniform(-1, 1, size=shape)
+            elif kind == "rm":
+                v = np.zeros(shape)
+            elif kind == "rv":
+                v = np.ones(shape)
+            elif kind == "nbt":
+                sd[name] = torch.tensor(0, dtype=torch.int64)
+                continue
+            elif kind == "emb":
+                v = rng.standard_normal(size=shape)
+            else:
+                raise ValueError(kind)
+            sd[name] = torch.tensor(np.asarray(v, dtype=np.float32).reshape(shape))
+        out[mod] = sd
+    return out
+
+
+# ----------------------------------------------------------------------------
+# layers (x is channel-first [B, C, N] like the reference's Conv1d inputs)
+# ----------------------------------------------------------------------------
+
+
+def conv(x, P, name):
+    return F.conv1d(x, P[name + ".weight"], P[name + ".bias"])
+
+
+def bn(x, P, name, training=True):
+    return F.batch_norm(x, P[name + ".running_mean"], P[name + ".running_var"],
+                        P[name + ".weight"], P[name + ".bias"], training, BN_MOMENTUM, BN_EPS)
+
+
+def target_encoder(P, x, sem_f, is_src, training=True):
+    """network/simple_encoder.py:88-107. x: [B,N,3] (tgt) or [B,P,N,3] (src)."""
+    if is_src:
+        B, Pn, N, _ = x.shape
+        x = x.reshape(B * Pn, N, 3)
+    N = x.shape[-2]
+    h = x.transpose(2, 1)
+    h = F.relu(bn(conv(h, P, "mlp1.0"), P, "mlp1.1", training))
+    h = F.relu(bn(conv(h, P, "mlp1.3"), P, "mlp1.4", training))
+    h = F.relu(bn(conv(h, P, "mlp2.0"), P, "mlp2.1", training))
+    h = F.relu(bn(conv(h, P, "mlp2.3"), P, "mlp2.4", training))
+    h = F.relu(bn(conv(h, P, "mlp2.6"), P, "mlp2.7", training))
+    if is_src:
+        s = sem_f.reshape(B * Pn, -1, 1).expand(-1, -1, N)
+    else:
+        s = sem_f.transpose(2, 1)
+    h = torch.cat([h, s], dim=1)
+    h = F.relu(bn(conv(h, P, "fuse_sem.0"), P, "fuse_sem.1", training))
+    pp = F.relu(bn(conv(h, P, "per_point_out.0"), P, "per_point_out.1", training))
+    pp = conv(pp, P, "per_point_out.3")
+    g = h.max(dim=2).values
+    g = F.linear(g, P["fc.weight"], P["fc.bias"])
+    return g, pp
+
+
+def ffn_norm(h, P, prefix, nlayers, use_bn, training=True):
+    i = 0
+    for _ in range(nlayers - 1):
+        h = F.relu(conv(h, P, f"{prefix}.{i}"))
+        if use_bn:
+            h = bn(h, P, f"{prefix}.{i + 2}", training)
+            i += 3
+        else:
+            i += 2
+    return conv(h, P, f"{prefix}.{i}")
+
+
+def residual_net(P, feat, training=True):
+    """network/deformation_net.py:102-107: feat [B,N,in] -> [B,N,3]."""
+    return ffn_norm(feat.permute(0, 2, 1), P, "residual_net", 4, True, training).permute(0, 2, 1)
+
+
+def _mha(P, p, q, kv, heads):
+    B, C, _ = q.shape
+    d = C // heads
+    Q = conv(q, P, p + ".in_proj_q").view(B, heads, d, -1)
+    K = conv(kv, P, p + ".in_proj_k").view(B, heads, d, -1)
+    V = conv(kv, P, p + ".in_proj_v").view(B, heads, d, -1)
+    att = torch.matmul(Q.transpose(2, 3), K) * d ** -0.5
+    att = att.softmax(dim=-1)
+    o = torch.matmul(att, V.transpose(2, 3)).transpose(2, 3).reshape(B, C, -1)
+    return conv(o, P, p + ".out_proj")
+
+
+def _prop(P, p, dq, dkv, heads, training):
+    msg = _mha(P, p + ".mha", dq, dkv, heads)
+    return dq + ffn_norm(torch.cat([dq, msg], dim=1), P, p + ".fc", 2, True, training)
+
+
+def deform_net(P, target_f, src_part_f, num_stages=2, heads=4, training=True):
+    """network/deformation_net.py:74-93 -> params [B, P, 6]."""
+    B = target_f.shape[0]
+    Pn = src_part_f.shape[1]
+    parts = src_part_f.reshape(B, Pn, -1).permute(0, 2, 1)
+    glob = torch.stack([parts.mean(dim=-1), target_f], dim=-1)
+    for L in range(2 * num_stages):
+        p = f"graph_attention_net.layers.{L}.module"
+        if L % 2 == 0:   # self attention, shared module for both node sets
+            glob, parts = _prop(P, p, glob, glob, heads, training), _prop(P, p, parts, parts, heads, training)
+        else:            # cross attention
+            g2 = _prop(P, p, glob, parts, heads, training)
+            parts = _prop(P, p, parts, g2, heads, training)
+            glob = g2
+    gr = torch.cat([glob[:, :, 0], glob[:, :, 1]], dim=1).unsqueeze(-1).expand(-1, -1, Pn)
+    full = torch.cat([gr, parts], dim=1)
+    return ffn_norm(full, P, "param_decoder", 2, False, training).permute(0, 2, 1).contiguous()
+
+
+# ----------------------------------------------------------------------------
+# geometry glue
+# ----------------------------------------------------------------------------
+
+
+def get_part(per_point, labels, x, max_parts):
+    """engine/train.py:103-136. per_point [B,N,C], labels [B,N] (float or int), x [B,N,3]."""
+    B = per_point.shape[0]
+    C = per_point.shape[-1]
+    target_part_f, re_in, part_x = [], [], []
+    mask = torch.zeros(B, max_parts)
+    param_def = torch.zeros(B, max_parts, 6)
+    for w in range(B):
+        feats, rows, px = [], [], []
+        for sem in torch.unique(labels[w]):
+            sel = labels[w] == sem
+            pts = x[w, sel]
+            px.append(pts)
+            lo, hi = pts.min(dim=0).values, pts.max(dim=0).values
+            param_def[w, int(sem)] = torch.cat([(lo + hi) / 2.0, (hi - lo) / 2.0])
+            f = per_point[w, sel]
+            m = f.mean(dim=0)
+            feats.append(m)
+            rows.append(torch.cat([f, m.unsqueeze(0).expand(f.shape[0], -1)], dim=-1))
+        k = len(feats)
+        padded = torch.zeros(max_parts, C, dtype=per_point.dtype)
+        padded = torch.cat([torch.stack(feats), padded[k:]], dim=0)
+        mask[w, :k] = 1
+        target_part_f.append(padded)
+        re_in.append(torch.cat(rows, dim=0))
+        part_x.append(px)
+    return torch.stack(target_part_f), torch.stack(re_in), mask, part_x, param_def
+
+
+def get_shape(A, param, default_param, weight):
+    """dataset/dataset_utils.py:691-726 (no connectivity, no param_init)."""
+    B, Pn, D = param.shape
+    A = A.reshape(B * Pn, -1, D)
+    p = weight * param.reshape(B * Pn, D, 1) + default_param.reshape(B * Pn, D, 1)
+    return torch.bmm(A, p).reshape(B, Pn, -1, 3)
+
+
+def get_symmetric(pc):
+    return torch.cat([-pc[:, :, :1], pc[:, :, 1:2], pc[:, :, 2:3]], dim=2)
+
+
+class _OracleNN(torch.autograd.Function):
+    """Chamfer primitive on the C oracle (values and idx bit-exact to the contract)."""
+
+    @staticmethod
+    def forward(ctx, p1, p2):
+        d1, d2, i1, i2 = nn_ref.nn_fwd(p1.detach().float().numpy(), p2.detach().float().numpy())
+        ctx.save_for_backward(p1, p2)
+        ctx.idx = (i1, i2)
+        return torch.from_numpy(d1).to(p1.dtype), torch.from_numpy(d2).to(p1.dtype)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        p1, p2 = ctx.saved_tensors
+        i1, i2 = ctx.idx
+        r1, r2 = nn_ref.nn_bwd(p1.detach().float().numpy(), p2.detach().float().numpy(),
+                               g1.float().numpy(), g2.float().numpy(), i1, i2)
+        return torch.from_numpy(r1).to(p1.dtype), torch.from_numpy(r2).to(p2.dtype)
+
+
+def chamfer_costs(p1, p2):
+    """Shape_Measure ChamferLoss stand-in: squared NN distances (cost1 [B,n], cost2 [B,m])."""
+    return _OracleNN.apply(p1, p2)
+
+
+def chamfer_distance2(p1, p2):
+    c1, c2 = chamfer_costs(p1, p2)
+    return c1.mean(dim=1) + c2.mean(dim=1)
+
+
+def compute_cm_loss(source_p, target_p, target_part, mask=None, np_per_part=1024):
+    if mask is None:
+        return chamfer_distance2(source_p, target_p)
+    n_valid = mask.sum(1) * np_per_part
+    full, part = [], []
+    for b in range(source_p.shape[0]):
+        full.append(chamfer_distance2(source_p[b:b + 1, :int(n_valid[b].item())], target_p[b:b + 1]))
+        lp = [chamfer_distance2(source_p[b:b + 1, i * np_per_part:(i + 1) * np_per_part], tp.unsqueeze(0))
+              for i, tp in enumerate(target_part[b])]
+        part.append(torch.stack(lp).mean())
+    return torch.stack(full).mean(), torch.stack(part).mean()
+
+
+def residual_retrieval_loss(x, x_source, residuals, mask, np_per_part=1024):
+    n_valid = mask.sum(1) * np_per_part
+    nns = []
+    for b in range(x.shape[0]):
+        src = x_source[b, :int(n_valid[b].item())].detach()
+        _, idx = nn_ref.nn_dir(x[b].detach().float().numpy(), src.float().numpy())
+        nns.append(src[torch.from_numpy(idx).long()])
+    nn = torch.stack(nns)
+    res = x + residuals - nn
+    return res.abs().sum(-1).mean(), residuals.abs().sum(-1).mean()
+
+
+def pc_consistency(a, b):
+    d = a - b
+    return (d * d).sum(-1).mean()
+
+
+def pc_consistency_weighted(a, b, mask):
+    d = a - b
+    per = (d * d).sum(-1).mean(-1)           # [B, P]
+    return (per * mask).sum() / mask.sum()
+
+
+def contrast_loss(tgt_part_f, src_f, src_labels, rank=0, gathered_src=None):
+    B, Pn = src_f.shape[0], src_f.shape[1]
+    t = F.normalize(tgt_part_f.reshape(B * Pn, -1), dim=-1, p=2)
+    s = F.normalize(src_f.reshape(B * Pn, -1), dim=-1, p=2)
+    labels = B * Pn * rank + torch.arange(B * Pn)
+    labels[src_labels.reshape(-1) == -1] = -1
+    s_all = s if gathered_src is None else gathered_src
+    scale = torch.tensor(math.log(1 / 0.07)).exp()
+    return F.cross_entropy(scale * t @ s_all.t(), labels, ignore_index=-1)
+
+
+# ----------------------------------------------------------------------------
+# the train step
+# ----------------------------------------------------------------------------
+
+LOSS_WEIGHTS_KEYS = ("use_chamfer_loss", "use_chamfer_part_loss", "use_contrast_loss",
+                     "use_symmetry_loss", "use_residuals_reg", "use_recon")
+
+
+def train_forward(params, batch, cfg, training=True, epoch=0):
+    """engine/train.py:204-335 on a synthetic batch dict (numpy/torch CPU tensors).
+
+    Returns (loss_all, terms dict). params: dict module -> state_dict (tensors may
+    require grad). BN running stats inside params are updated in place (training).
+    """
+    P_max = cfg["MAX_NUM_PARTS"]
+    emb = params["embedding_layer"]["weight"]
+    src_idx = batch["src_index"]                          # [B,P] (already -1 -> last source)
+    src_pts = batch["src_points"][src_idx]                # [B,P,1024,3]
+    mats = batch["src_mats"][src_idx]                     # [B,P,3072,6]
+    src_sem_f = emb[batch["src_sem"][src_idx]]
+    tgt_sem_f = emb[batch["tgt_sem"]]
+    x = batch["x"]
+    B = x.shape[0]
+
+    codes, src_pp = target_encoder(params["src_encoder_all"], src_pts, src_sem_f, True, training)
+    rin = torch.cat([codes.unsqueeze(2).expand(-1, -1, src_pp.shape[-1]), src_pp], dim=1)
+    recon_src = residual_net(params["recon_decoder_src"], rin.permute(0, 2, 1), training)
+    recon_src = recon_src.reshape(B, P_max, -1, 3)
+
+    tcode, pp = target_encoder(params["target_encoder_full"], x, tgt_sem_f, False, training)
+    pp = pp.permute(0, 2, 1)
+    part_f, re_in, mask, part_x, param_def = get_part(pp, batch["labels"], x, P_max)
+    N = pp.shape[1]
+    recon_full = residual_net(params["recon_decoder_full"],
+                              torch.cat([pp, tcode.unsqueeze(1).expand(-1, N, -1)], dim=-1), training)
+    re_res = residual_net(params["re_residual_net_full"], re_in, training)
+    codes = codes.reshape(B, P_max, -1)
+    prm = deform_net(params["param_decoder_full"], tcode, codes, training=training)
+    out = get_shape(mats, prm, param_def, cfg["alpha"]).reshape(B, -1, 3)
+
+    T = OrderedDict()
+    T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask)
+    T["contrast_loss"] = contrast_loss(part_f, codes, batch["src_labels"])
+    T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(get_symmetric(out), x, part_x, mask)
+    if epoch > cfg["init_p_m_loss"]:
+        T["re_reg_loss_full"], T["reg_loss_full"] = residual_retrieval_loss(x, out.detach(), re_res, mask)
+    T["recon_loss_full"] = pc_consistency(recon_full, x)
+    T["recon_loss_src"] = pc_consistency_weighted(recon_src, src_pts, mask)
+    loss = (T["cd_loss_full"] * cfg["use_chamfer_loss"] + T["cd_loss_part"] * cfg["use_chamfer_part_loss"]
+            + T["contrast_loss"] * cfg["use_contrast_loss"] + T["ref_cd_loss_full"] * cfg["use_symmetry_loss"])
+    if "re_reg_loss_full" in T:
+        loss = loss + T["re_reg_loss_full"] * cfg["use_residuals_reg"] + T["reg_loss_full"] * cfg["use_residuals_reg"] * 0.01
+    loss = loss + T["recon_loss_full"] * cfg["use_recon"] + T["recon_loss_src"] * cfg["use_recon"]
+    T["all_loss"] = loss
+    T["_out"] = out
+    T["_params"] = prm
+    return loss, T
+
+
+TRAINED_MODULES = ("target_encoder_full", "param_decoder_full", "re_residual_net_full",
+                   "recon_decoder_full", "src_encoder_all", "recon_decoder_src")
+
+
+def trainable(params):
+    """The tensors that the reference hands to Adam (embedding excluded) in its order."""
+    out = []
+    for mod in TRAINED_MODULES:
+        for k, v in params[mod].items():
+            if v.dtype.is_floating_point and not (k.endswith("running_mean") or k.endswith("running_var")):
+                out.append((mod, k, v))
+    return out

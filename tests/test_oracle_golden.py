@@ -1,0 +1,177 @@
+"""Pin the oracle (CPU restatement) against golden vectors generated from the
+reference itself (tests/golden/make_golden.py). CPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import nn_ref, ured_ref
+
+CFG = {"source_latent_dim": 64, "target_latent_dim": 64, "sem_latent_dim": 16, "MAX_NUM_PARTS": 16,
+       "alpha": 0.1, "use_chamfer_loss": 30.0, "use_chamfer_part_loss": 1.0, "use_symmetry_loss": 30.0,
+       "use_contrast_loss": 0.5, "use_param_loss": 0.0, "init_p_m_loss": -1, "use_residuals_reg": 3.0,
+       "use_recon": 30.0}
+SEED = 7
+
+
+def _g(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def test_nn_oracle_vs_distchamfer():
+    """chamfer_python.distChamfer is the reference's own oracle (unit_test.py:14-35):
+    MSE < 1e-8 and exact index equality on random data."""
+    g = _g("nn_distchamfer.npz")
+    for case in ("u4x100x200", "u3x257x129", "u2x1x5", "u1x2048x2048"):
+        d1, d2, i1, i2 = nn_ref.nn_fwd(g[case + "/p1"], g[case + "/p2"])
+        assert np.mean((d1 - g[case + "/d1"]) ** 2) + np.mean((d2 - g[case + "/d2"]) ** 2) < 1e-8
+        assert np.abs(d1 - g[case + "/d1"]).max() < 1e-6 and np.abs(d2 - g[case + "/d2"]).max() < 1e-6
+        np.testing.assert_array_equal(i1, g[case + "/i1"])
+        np.testing.assert_array_equal(i2, g[case + "/i2"])
+
+
+def _direct_sq(q, r):
+    q = q.astype(np.float32); r = r.astype(np.float32)
+    dx = r[None, :, 0] - q[:, None, 0]; dy = r[None, :, 1] - q[:, None, 1]; dz = r[None, :, 2] - q[:, None, 2]
+    inner = (dy.astype(np.float64) * dy + (dx * dx).astype(np.float64)).astype(np.float32)  # fmaf(dy,dy,dx*dx)
+    return (dz.astype(np.float64) * dz + inner.astype(np.float64)).astype(np.float32)      # fmaf(dz,dz,inner)
+
+
+def test_nn_oracle_ties_lowest_index():
+    """Grid refs with exact fp32 ties: the reference keeps the first minimum (strict '<', chamfer3D.cu:36-69)."""
+    g = _g("nn_distchamfer.npz")
+    q, r = g["grid/p1"][0], g["grid/p2"][0]
+    d, i = nn_ref.nn_dir(q, r)
+    D = _direct_sq(q, r)
+    assert np.abs(d - g["grid/d1"][0]).max() < 1e-6
+    for j in range(q.shape[0]):
+        assert D[j, i[j]] == d[j]
+        assert i[j] == np.flatnonzero(D[j] == D[j].min())[0]
+    assert (np.sum(D == D.min(axis=1, keepdims=True), axis=1) > 1).sum() >= 300  # the tie cases exist
+
+
+def _req(P):
+    for k, v in P.items():
+        if v.dtype.is_floating_point and "running" not in k:
+            v.requires_grad_(True)
+
+
+def _params():
+    return ured_ref.make_params(CFG, seed=SEED)
+
+
+def test_target_encoder_golden():
+    g = _g("modules.npz")
+    P = _params()["target_encoder_full"]
+    _req(P)
+    x = torch.tensor(g["tgt/x"], requires_grad=True)
+    s = torch.tensor(g["tgt/sem"], requires_grad=True)
+    code, pp = ured_ref.target_encoder(P, x, s, False)
+    np.testing.assert_allclose(code.detach().numpy(), g["tgt/code"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(pp.detach().numpy(), g["tgt/pp"], rtol=1e-4, atol=1e-5)
+    ((code * torch.tensor(g["tgt/w1"])).sum() + (pp * torch.tensor(g["tgt/w2"])).sum()).backward()
+    np.testing.assert_allclose(x.grad.numpy(), g["tgt/gx"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(s.grad.numpy(), g["tgt/gsem"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(P["fuse_sem.0.weight"].grad[:32].numpy(), g["tgt/g_fuse_w"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(P["mlp1.0.weight"].grad.numpy(), g["tgt/g_mlp10_w"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(P["per_point_out.3.weight"].grad.numpy(), g["tgt/g_ppo3_w"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(P["fc.weight"].grad.numpy(), g["tgt/g_fc_w"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(P["fuse_sem.1.running_mean"].detach().numpy(), g["tgt/rm_fuse"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(P["fuse_sem.1.running_var"].detach().numpy(), g["tgt/rv_fuse"], rtol=1e-4, atol=1e-6)
+    with torch.no_grad():
+        c_e, pp_e = ured_ref.target_encoder(P, x, s, False, training=False)
+    np.testing.assert_allclose(c_e.numpy(), g["tgt_eval/code"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(pp_e.numpy(), g["tgt_eval/pp"], rtol=1e-4, atol=1e-5)
+
+
+def test_source_encoder_golden():
+    g = _g("modules.npz")
+    P = _params()["src_encoder_all"]
+    code, pp = ured_ref.target_encoder(P, torch.tensor(g["src/x"]), torch.tensor(g["src/sem"]), True)
+    np.testing.assert_allclose(code.detach().numpy(), g["src/code"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(pp.detach().numpy(), g["src/pp"], rtol=1e-4, atol=1e-5)
+
+
+def test_residual_net_golden():
+    g = _g("modules.npz")
+    P = _params()["recon_decoder_full"]
+    _req(P)
+    f = torch.tensor(g["res/in"], requires_grad=True)
+    r = ured_ref.residual_net(P, f)
+    np.testing.assert_allclose(r.detach().numpy(), g["res/out"], rtol=1e-4, atol=1e-5)
+    (r * torch.tensor(g["res/w"])).sum().backward()
+    np.testing.assert_allclose(f.grad.numpy(), g["res/gin"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(P["residual_net.0.weight"].grad.numpy(), g["res/g_w0"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(P["residual_net.9.weight"].grad.numpy(), g["res/g_w9"], rtol=1e-3, atol=1e-5)
+
+
+def test_deform_net_golden():
+    g = _g("modules.npz")
+    P = _params()["param_decoder_full"]
+    _req(P)
+    tf = torch.tensor(g["dn/tf"], requires_grad=True)
+    spf = torch.tensor(g["dn/spf"], requires_grad=True)
+    prm = ured_ref.deform_net(P, tf, spf)
+    np.testing.assert_allclose(prm.detach().numpy(), g["dn/params"], rtol=1e-4, atol=1e-5)
+    (prm * torch.tensor(g["dn/w"])).sum().backward()
+    np.testing.assert_allclose(tf.grad.numpy(), g["dn/gtf"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(spf.grad.numpy(), g["dn/gspf"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(P["param_decoder.0.weight"].grad.numpy(), g["dn/g_dec0_w"], rtol=1e-3, atol=1e-5)
+
+
+def test_small_losses_golden():
+    g = _g("modules.npz")
+    a, b, m = torch.tensor(g["cons/a"]), torch.tensor(g["cons/b"]), torch.tensor(g["cons/mask"])
+    np.testing.assert_allclose(ured_ref.pc_consistency(a[:, 0], b[:, 0]).numpy(), g["cons/plain"], rtol=1e-6)
+    np.testing.assert_allclose(ured_ref.pc_consistency_weighted(a, b, m).numpy(), g["cons/weighted"], rtol=1e-6)
+    loss = ured_ref.contrast_loss(torch.tensor(g["con/t"]), torch.tensor(g["con/s"]), torch.tensor(g["con/l"]))
+    np.testing.assert_allclose(loss.numpy(), g["con/loss"], rtol=1e-6)
+
+
+def synthetic_step_batch():
+    from dataset import synthetic
+    db = synthetic.make_source_db(24, seed=3)
+    bt = synthetic.make_batch(2, 128, 24, max_parts=16, parts=[3, 2], seed=4)
+    batch = {"src_points": torch.from_numpy(db["src_points"]), "src_mats": torch.from_numpy(db["src_mats"]),
+             "src_sem": torch.from_numpy(db["src_sem"]), "src_index": torch.from_numpy(bt["src_index"]),
+             "tgt_sem": torch.from_numpy(bt["tgt_sem"]), "x": torch.from_numpy(bt["x"]),
+             "labels": torch.from_numpy(bt["labels"]).float(), "src_labels": torch.from_numpy(bt["src_labels"])}
+    return batch
+
+
+def test_train_step_golden():
+    """The whole engine/train.py:204-338 step (reference functions composed) vs the oracle."""
+    g = _g("train_step.npz")
+    P = _params()
+    for mod in P.values():
+        for k, v in mod.items():
+            if v.dtype.is_floating_point and not ("running" in k):
+                v.requires_grad_(True)
+    batch = synthetic_step_batch()
+    loss, T = ured_ref.train_forward(P, batch, dict(CFG, batch_size=2))
+    np.testing.assert_allclose(T["_out"].detach().numpy(), g["out"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(T["_params"].detach().numpy(), g["params_full"], rtol=1e-4, atol=1e-5)
+    for k in ("cd_loss_full", "cd_loss_part", "contrast_loss", "ref_cd_loss_full", "ref_cd_loss_part",
+              "re_reg_loss_full", "reg_loss_full", "recon_loss_full", "recon_loss_src", "all_loss"):
+        np.testing.assert_allclose(T[k].detach().numpy(), g["loss/" + k], rtol=2e-5, err_msg=k)
+    loss.backward()
+    nchecked = 0
+    for key in g.files:
+        if not key.startswith("gnorm/"):
+            continue
+        _, mod, name = key.split("/", 2)
+        got = P[mod][name].grad
+        assert got is not None, key
+        # conv biases that feed a training-mode BN have ~0 true gradient (BN cancels them):
+        # their norms are rounding noise, hence the absolute floor
+        np.testing.assert_allclose(got.norm().item(), g[key], rtol=2e-3, atol=1e-4, err_msg=key)
+        nchecked += 1
+    assert nchecked > 150
+    np.testing.assert_allclose(P["param_decoder_full"]["param_decoder.2.weight"].grad.numpy(),
+                               g["g/param_decoder.2.weight"], rtol=2e-3, atol=1e-5)
+    np.testing.assert_allclose(P["recon_decoder_src"]["residual_net.9.weight"].grad.numpy(),
+                               g["g/recon_src.9.weight"], rtol=2e-3, atol=1e-5)
+    np.testing.assert_allclose(P["re_residual_net_full"]["residual_net.9.weight"].grad.numpy(),
+                               g["g/re_res.9.weight"], rtol=2e-3, atol=1e-5)
