@@ -1,0 +1,768 @@
+// mlp.hip — per-point MLP (Conv1d k=1 + BatchNorm1d + ReLU) for MI355X / gfx950.
+//
+// Replaces the 1x1-conv chains of TargetEncoder (network/simple_encoder.py:52-107)
+// and re_residual_net / FeedForwardNet_norm (network/deformation_net.py:96-107,
+// attention_graph/attention_utils.py:62-86), forward and backward.
+//
+// Activations are point-major [M][C] (C contiguous), so a 1x1 conv is the GEMM
+// Y = X W^T with M = points (up to 262,144 here), N = Cout, K = Cin. The GEMM
+// runs on v_mfma_f32_32x32x2_f32 (fp32 in, fp32 accumulate, exact fma chains).
+//
+//  * block tile 128x128, BK = 32, 256 threads = 2x2 waves, each wave 64x64 =
+//    2x2 MFMA 32x32 tiles (64 accumulator registers);
+//  * LDS holds both operands reduction-major (As[k][m], Bs[k][n]) so every
+//    MFMA operand is one conflict-free ds_read_b32 per lane; row-major global
+//    operands are transposed on the LDS write (row pad 1 -> conflict-free
+//    ds_write_b32), k-major ones are copied (pad 4 -> ds_write_b128);
+//  * the next K-tile is prefetched into registers while the current one is
+//    consumed (T14 split: issue early, write LDS after the barrier);
+//  * fused prologue: the previous layer's BatchNorm + ReLU is applied while
+//    staging the operand (relu(x*s+t) or relu(x)*s+t), so normalised
+//    activations are never written to HBM;
+//  * fused epilogues: bias / per-group row bias, BN batch-statistics partials
+//    (per-block mean & M2, merged in fp64 by ured_bn_fwd_finalize — Chan's
+//    parallel variance, order-fixed, deterministic), max-pool partials, the
+//    BN-backward masks/partials of the previous layer, or split-K partials;
+//  * XCD-aware tile order: blocks that share an A row-panel run on one XCD.
+#include "ured_common.h"
+#include "../../include/ured_hip.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+struct Gemm {
+    UredGemmDesc d;
+};
+
+__device__ __forceinline__ float pro_apply(int pro, float x, float s, float t) {
+    if (pro == URED_PRO_ENC) return fmaxf(__builtin_fmaf(x, s, t), 0.f);
+    if (pro == URED_PRO_RES) return __builtin_fmaf(fmaxf(x, 0.f), s, t);
+    return x;
+}
+
+// XCD-aware bijective remap of a linear block id (blocks b and b+8 share an XCD).
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg / 8, r = nwg % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// ---- operand staging -------------------------------------------------------
+// A "row-major" operand tile: ROWS (m or n) x BK (k) from G[row*ld + k]; k contiguous.
+// Staged into LDS transposed: S[k][row] with row stride LDP.
+// Thread t handles k4 = t % 8 (4 consecutive k) and rows t/8 + 32*i, i = 0..3.
+struct RowTile { float v[4][4]; };
+
+template <int PRO>
+__device__ __forceinline__ void load_rowmajor(RowTile& r, const float* __restrict__ G, int ld, int rows, int row0,
+                                              int K, int k0, const float* __restrict__ A2, int ld2, int k1,
+                                              const float* __restrict__ ps, const float* __restrict__ pt,
+                                              bool vec) {
+    const int t = threadIdx.x, k4 = t & 7;
+    const int kb = k0 + 4 * k4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = row0 + (t >> 3) + 32 * i;
+        float x[4] = {0.f, 0.f, 0.f, 0.f};
+        if (row < rows) {
+            if (vec && kb + 3 < K && (kb + 3 < k1 || kb >= k1)) {
+                if (kb < k1) {
+                    const float4 q = *reinterpret_cast<const float4*>(G + (size_t)row * ld + kb);
+                    x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+                    if (PRO != URED_PRO_NONE) {
+                        const float4 s = *reinterpret_cast<const float4*>(ps + kb);
+                        const float4 tt = *reinterpret_cast<const float4*>(pt + kb);
+                        x[0] = pro_apply(PRO, x[0], s.x, tt.x); x[1] = pro_apply(PRO, x[1], s.y, tt.y);
+                        x[2] = pro_apply(PRO, x[2], s.z, tt.z); x[3] = pro_apply(PRO, x[3], s.w, tt.w);
+                    }
+                } else {
+                    const float4 q = *reinterpret_cast<const float4*>(A2 + (size_t)row * ld2 + (kb - k1));
+                    x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int k = kb + c;
+                    if (k < K) {
+                        if (k < k1) {
+                            float v = G[(size_t)row * ld + k];
+                            if (PRO != URED_PRO_NONE) v = pro_apply(PRO, v, ps[k], pt[k]);
+                            x[c] = v;
+                        } else {
+                            x[c] = A2[(size_t)row * ld2 + (k - k1)];
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) r.v[i][c] = x[c];
+    }
+}
+
+template <int LDP>
+__device__ __forceinline__ void store_rowmajor(const RowTile& r, float* S) {
+    const int t = threadIdx.x, k4 = t & 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = (t >> 3) + 32 * i;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) S[(4 * k4 + c) * LDP + row] = r.v[i][c];
+    }
+}
+
+// A "k-major" operand tile: BK (k) x COLS (m or n) from G[k*ld + col]; col contiguous.
+// Staged directly: S[k][col]. Thread t handles col4 = t % 32 and k = t/32 + 8*i.
+template <int PRO>
+__device__ __forceinline__ void load_kmajor(RowTile& r, const float* __restrict__ G, int ld, int cols, int col0,
+                                            int K, int k0, const float* __restrict__ ps,
+                                            const float* __restrict__ pt, bool vec) {
+    const int t = threadIdx.x, c4 = t & 31;
+    const int cb = col0 + 4 * c4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = k0 + (t >> 5) + 8 * i;
+        float x[4] = {0.f, 0.f, 0.f, 0.f};
+        if (k < K) {
+            if (vec && cb + 3 < cols) {
+                const float4 q = *reinterpret_cast<const float4*>(G + (size_t)k * ld + cb);
+                x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+                if (PRO != URED_PRO_NONE) {
+                    const float4 s = *reinterpret_cast<const float4*>(ps + cb);
+                    const float4 tt = *reinterpret_cast<const float4*>(pt + cb);
+                    x[0] = pro_apply(PRO, x[0], s.x, tt.x); x[1] = pro_apply(PRO, x[1], s.y, tt.y);
+                    x[2] = pro_apply(PRO, x[2], s.z, tt.z); x[3] = pro_apply(PRO, x[3], s.w, tt.w);
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int col = cb + c;
+                    if (col < cols) {
+                        float v = G[(size_t)k * ld + col];
+                        if (PRO != URED_PRO_NONE) v = pro_apply(PRO, v, ps[col], pt[col]);
+                        x[c] = v;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) r.v[i][c] = x[c];
+    }
+}
+
+template <int LDP>
+__device__ __forceinline__ void store_kmajor(const RowTile& r, float* S) {
+    const int t = threadIdx.x, c4 = t & 31;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = (t >> 5) + 8 * i;
+        *reinterpret_cast<float4*>(S + k * LDP + 4 * c4) = make_float4(r.v[i][0], r.v[i][1], r.v[i][2], r.v[i][3]);
+    }
+}
+
+template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; };
+
+// ---- the kernel ---------------------------------------------------------------
+template <bool A_KM, bool B_KM, int PRO_A, int PRO_B, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
+    constexpr int LDA = Pad<A_KM>::v, LDB = Pad<B_KM>::v;
+    __shared__ __attribute__((aligned(16))) float As[BK * LDA];
+    __shared__ __attribute__((aligned(16))) float Bs[BK * LDB];
+    __shared__ float red[2][2][BN];       // [wm][quantity][col] cross-wave reductions
+    __shared__ int redi[2][2][BN];
+
+    const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
+    const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+    const int tm_ = tile / ntn, tn_ = tile % ntn;
+    const int m0 = tm_ * BM, n0 = tn_ * BN;
+    int kbeg = 0, kend = d.K;
+    if (EPI == URED_EPI_SPLITK) {
+        const int kps = ((d.K + d.splits - 1) / d.splits + BK - 1) / BK * BK;
+        kbeg = blockIdx.z * kps;
+        kend = min(d.K, kbeg + kps);
+    }
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
+    const bool vecA = ((d.lda & 3) == 0) && (A_KM || ((d.k1 & 3) == 0 && (d.A2 == nullptr || (d.lda2 & 3) == 0)));
+    const bool vecB = (d.ldb & 3) == 0;
+
+    f16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    RowTile ra, rb;
+    auto load = [&](int k0) {
+        if (A_KM) load_kmajor<PRO_A>(ra, d.A, d.lda, d.M, m0, kend, k0, d.pro_s, d.pro_t, vecA);
+        else load_rowmajor<PRO_A>(ra, d.A, d.lda, d.M, m0, kend, k0, d.A2, d.lda2, d.k1, d.pro_s, d.pro_t, vecA);
+        if (B_KM) load_kmajor<PRO_B>(rb, d.B, d.ldb, d.N, n0, kend, k0, d.pro_s, d.pro_t, vecB);
+        else load_rowmajor<URED_PRO_NONE>(rb, d.B, d.ldb, d.N, n0, kend, k0, nullptr, 0, 0x7fffffff, nullptr, nullptr, vecB);
+    };
+    auto stage = [&]() {
+        if (A_KM) store_kmajor<LDA>(ra, As); else store_rowmajor<LDA>(ra, As);
+        if (B_KM) store_kmajor<LDB>(rb, Bs); else store_rowmajor<LDB>(rb, Bs);
+    };
+
+    if (kbeg < kend) {
+        load(kbeg);
+        for (int k0 = kbeg; k0 < kend; k0 += BK) {
+            __syncthreads();
+            stage();
+            __syncthreads();
+            if (k0 + BK < kend) load(k0 + BK);   // prefetch: latency hidden under the MFMAs
+            const float* ap = As + (lane >> 5) * LDA + wm * 64 + (lane & 31);
+            const float* bp = Bs + (lane >> 5) * LDB + wn * 64 + (lane & 31);
+#pragma unroll
+            for (int kk = 0; kk < BK / 2; ++kk) {
+                const float a0 = ap[2 * kk * LDA], a1 = ap[2 * kk * LDA + 32];
+                const float b0 = bp[2 * kk * LDB], b1 = bp[2 * kk * LDB + 32];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            }
+        }
+    }
+
+    // ---- epilogues --------------------------------------------------------------
+    // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
+    const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
+    auto row_of = [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); };
+
+    if (EPI == URED_EPI_STORE || EPI == URED_EPI_SPLITK) {
+        float* C = d.C + (EPI == URED_EPI_SPLITK ? (size_t)blockIdx.z * d.M * d.ldc : 0);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+            if (col >= d.N) continue;
+            const float bsv = (EPI == URED_EPI_STORE && d.bias) ? d.bias[col] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = row_of(i, r);
+                    if (row < d.M) C[(size_t)row * d.ldc + col] = acc[i][j][r] + bsv;
+                }
+        }
+        return;
+    }
+
+    const int blk = m0 / BM;
+    const int nvalid = min(BM, d.M - m0);
+
+    if (EPI == URED_EPI_FWD) {
+        // value, store, per-column block stats (two-pass on registers: mean then M2)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+            const bool cv = col < d.N;
+            const float bsv = (cv && d.bias) ? d.bias[col] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = row_of(i, r);
+                    float v = acc[i][j][r] + bsv;
+                    if (cv && row < d.M) {
+                        if (d.rowbias) {
+                            const int g = d.gidx ? d.gidx[row] : row / d.group_rows;
+                            v += d.rowbias[(size_t)g * d.ldr + col];
+                        }
+                        d.C[(size_t)row * d.ldc + col] = v;
+                    }
+                    acc[i][j][r] = v;
+                }
+        }
+        // pass 1: column sums of p over valid rows
+        float csum[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float p = d.stat_relu ? fmaxf(acc[i][j][r], 0.f) : acc[i][j][r];
+                    s += (row_of(i, r) < d.M) ? p : 0.f;
+                }
+            s += __shfl_xor(s, 32);
+            csum[j] = s;
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) red[wm][0][wn * 64 + j * 32 + lane] = csum[j];
+        }
+        __syncthreads();
+        float cmean[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = wn * 64 + j * 32 + (lane & 31);
+            cmean[j] = (red[0][0][c] + red[1][0][c]) / (float)nvalid;
+        }
+        // pass 2: M2 about the block mean
+        float cm2[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float p = d.stat_relu ? fmaxf(acc[i][j][r], 0.f) : acc[i][j][r];
+                    const float e = p - cmean[j];
+                    s += (row_of(i, r) < d.M) ? e * e : 0.f;
+                }
+            s += __shfl_xor(s, 32);
+            cm2[j] = s;
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) red[wm][1][wn * 64 + j * 32 + lane] = cm2[j];
+        }
+        __syncthreads();
+        if (wm == 0 && lane < 32) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int c = wn * 64 + j * 32 + lane;
+                const int col = n0 + c;
+                if (col < d.N) {
+                    d.stat_ws[(size_t)blk * 2 * d.N + col] = cmean[j];
+                    d.stat_ws[(size_t)blk * 2 * d.N + d.N + col] = red[0][1][c] + red[1][1][c];
+                }
+            }
+        }
+        if (d.pool_ws) {
+            __syncthreads();
+            // per column max/min of Y with lowest-row tie break
+            float mx[2], mn[2];
+            int ix[2], in_[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                mx[j] = -__builtin_inff(); mn[j] = __builtin_inff(); ix[j] = 0x7fffffff; in_[j] = 0x7fffffff;
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = row_of(i, r);
+                        if (row >= d.M) continue;
+                        const float v = acc[i][j][r];
+                        if (v > mx[j] || (v == mx[j] && row < ix[j])) { mx[j] = v; ix[j] = row; }
+                        if (v < mn[j] || (v == mn[j] && row < in_[j])) { mn[j] = v; in_[j] = row; }
+                    }
+                const float omx = __shfl_xor(mx[j], 32), omn = __shfl_xor(mn[j], 32);
+                const int oix = __shfl_xor(ix[j], 32), oin = __shfl_xor(in_[j], 32);
+                if (omx > mx[j] || (omx == mx[j] && oix < ix[j])) { mx[j] = omx; ix[j] = oix; }
+                if (omn < mn[j] || (omn == mn[j] && oin < in_[j])) { mn[j] = omn; in_[j] = oin; }
+            }
+            if (lane < 32) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int c = wn * 64 + j * 32 + lane;
+                    red[wm][0][c] = mx[j]; redi[wm][0][c] = ix[j];
+                    red[wm][1][c] = mn[j]; redi[wm][1][c] = in_[j];
+                }
+            }
+            __syncthreads();
+            if (wm == 0 && lane < 32) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int c = wn * 64 + j * 32 + lane;
+                    const int col = n0 + c;
+                    if (col >= d.N) continue;
+                    float a = red[0][0][c]; int ai = redi[0][0][c];
+                    if (red[1][0][c] > a || (red[1][0][c] == a && redi[1][0][c] < ai)) { a = red[1][0][c]; ai = redi[1][0][c]; }
+                    float b = red[0][1][c]; int bi = redi[0][1][c];
+                    if (red[1][1][c] < b || (red[1][1][c] == b && redi[1][1][c] < bi)) { b = red[1][1][c]; bi = redi[1][1][c]; }
+                    float* pw = d.pool_ws + (size_t)blk * 4 * d.N;
+                    pw[col] = a; reinterpret_cast<int*>(pw)[d.N + col] = ai;
+                    pw[2 * d.N + col] = b; reinterpret_cast<int*>(pw)[3 * d.N + col] = bi;
+                }
+            }
+        }
+        return;
+    }
+
+    if (EPI == URED_EPI_BNBWD) {
+        float s1[2], s2[2];
+        // max-pool backward: the pooled gradient lands on the winning row of each (group, column)
+        const bool pool_blk = d.pool_idx && (d.pool_group_rows % BM == 0);
+        const int pg = pool_blk ? m0 / d.pool_group_rows : 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+            const bool cv = col < d.N;
+            const int cc = cv ? col : 0;
+            const float sc = d.bn_scale[cc], sh = d.bn_shift[cc], mu = d.bn_mean[cc], is = d.bn_invstd[cc];
+            int pidx = -1; float pgr = 0.f;
+            if (pool_blk && cv) { pidx = d.pool_idx[(size_t)pg * d.N + col]; pgr = d.pool_grad[(size_t)pg * d.N + col]; }
+            float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = row_of(i, r);
+                    if (!cv || row >= d.M) continue;
+                    float dh = acc[i][j][r];
+                    if (pool_blk) {
+                        if (row == pidx) dh += pgr;
+                    } else if (d.pool_idx) {
+                        const size_t ge = (size_t)(row / d.pool_group_rows) * d.N + col;
+                        if (d.pool_idx[ge] == row) dh += d.pool_grad[ge];
+                    }
+                    const float y = d.Yp[(size_t)row * d.ldy + col];
+                    float g, xh;
+                    if (d.bwd_res) {
+                        g = dh;
+                        xh = (fmaxf(y, 0.f) - mu) * is;
+                    } else {
+                        g = (__builtin_fmaf(y, sc, sh) > 0.f) ? dh : 0.f;
+                        xh = (y - mu) * is;
+                    }
+                    d.C[(size_t)row * d.ldc + col] = g;
+                    a1 += g;
+                    a2 += g * xh;
+                }
+            a1 += __shfl_xor(a1, 32);
+            a2 += __shfl_xor(a2, 32);
+            s1[j] = a1; s2[j] = a2;
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                red[wm][0][wn * 64 + j * 32 + lane] = s1[j];
+                red[wm][1][wn * 64 + j * 32 + lane] = s2[j];
+            }
+        }
+        __syncthreads();
+        if (wm == 0 && lane < 32) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int c = wn * 64 + j * 32 + lane;
+                const int col = n0 + c;
+                if (col < d.N) {
+                    d.bwd_ws[(size_t)blk * 2 * d.N + col] = red[0][0][c] + red[1][0][c];
+                    d.bwd_ws[(size_t)blk * 2 * d.N + d.N + col] = red[0][1][c] + red[1][1][c];
+                }
+            }
+        }
+    }
+}
+
+// ---- small kernels -------------------------------------------------------------
+
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                     float* __restrict__ out, int ldo, int accumulate) {
+    const size_t total = (size_t)M * N;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int m = e / N, n = e % N;
+        float s = 0.f;
+        for (int z = 0; z < splits; ++z) s += ws[(size_t)z * total + e];
+        float* o = out + (size_t)m * ldo + n;
+        *o = accumulate ? *o + s : s;
+    }
+}
+
+// one block (256 threads) per column; fp64 fixed-order tree reductions
+__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ ws, int M, int N,
+        const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+        float* running_mean, float* running_var, float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
+    __shared__ double sh[256];
+    const int n = blockIdx.x, t = threadIdx.x;
+    const int nblk = (M + BM - 1) / BM;
+    double s = 0.0;
+    for (int b = t; b < nblk; b += 256) {
+        const int cnt = min(BM, M - b * BM);
+        s += (double)cnt * (double)ws[(size_t)b * 2 * N + n];
+    }
+    sh[t] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) { if (t < o) sh[t] += sh[t + o]; __syncthreads(); }
+    const double mean = sh[0] / (double)M;
+    __syncthreads();
+    double q = 0.0;
+    for (int b = t; b < nblk; b += 256) {
+        const int cnt = min(BM, M - b * BM);
+        const double dm = (double)ws[(size_t)b * 2 * N + n] - mean;
+        q += (double)ws[(size_t)b * 2 * N + N + n] + (double)cnt * dm * dm;
+    }
+    sh[t] = q;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) { if (t < o) sh[t] += sh[t + o]; __syncthreads(); }
+    if (t == 0) {
+        const double m2 = sh[0];
+        const double var = m2 / (double)M;
+        const float is = (float)(1.0 / sqrt(var + (double)eps));
+        const float mf = (float)mean;
+        mean_o[n] = mf;
+        invstd_o[n] = is;
+        const float sc = gamma ? gamma[n] * is : is;
+        scale_o[n] = sc;
+        shift_o[n] = (beta ? beta[n] : 0.f) - mf * sc;
+        if (running_mean) running_mean[n] = (1.f - momentum) * running_mean[n] + momentum * mf;
+        if (running_var) {
+            const float uv = (float)(M > 1 ? m2 / (double)(M - 1) : m2);
+            running_var[n] = (1.f - momentum) * running_var[n] + momentum * uv;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ ws, int M, int N,
+        const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma, float* dbeta, int accumulate,
+        float* ca, float* cb, float* cc) {
+    __shared__ double s1[256], s2[256];
+    const int n = blockIdx.x, t = threadIdx.x;
+    const int nblk = (M + BM - 1) / BM;
+    double a = 0.0, b = 0.0;
+    for (int k = t; k < nblk; k += 256) {
+        a += (double)ws[(size_t)k * 2 * N + n];
+        b += (double)ws[(size_t)k * 2 * N + N + n];
+    }
+    s1[t] = a; s2[t] = b;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) { s1[t] += s1[t + o]; s2[t] += s2[t + o]; }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const double db = s1[0], dg = s2[0];
+        if (dbeta) dbeta[n] = accumulate ? dbeta[n] + (float)db : (float)db;
+        if (dgamma) dgamma[n] = accumulate ? dgamma[n] + (float)dg : (float)dg;
+        const double is = invstd[n];
+        const double k = (gamma ? (double)gamma[n] : 1.0) * is;
+        ca[n] = (float)k;
+        cb[n] = (float)(-k * is * dg / (double)M);
+        cc[n] = (float)(-k * db / (double)M);
+    }
+}
+
+// rows in blocks of 128 (matches the partial layout), 256 threads = columns
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ G, const float* __restrict__ Y,
+        int M, int N, int ld, int res, const float* __restrict__ mean, const float* __restrict__ ca,
+        const float* __restrict__ cb, const float* __restrict__ cc, float* __restrict__ dY, float* __restrict__ colsum) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    const int blk = blockIdx.y;
+    if (n >= N) return;
+    const float a = ca[n], b = cb[n], c = cc[n], mu = mean[n];
+    const int r0 = blk * BM, r1 = min(M, r0 + BM);
+    float s = 0.f;
+    for (int r = r0; r < r1; ++r) {
+        const size_t e = (size_t)r * ld + n;
+        const float y = Y[e];
+        const float p = res ? fmaxf(y, 0.f) : y;
+        float v = __builtin_fmaf(a, G[e], __builtin_fmaf(b, p - mu, c));
+        if (res && !(y > 0.f)) v = 0.f;
+        dY[e] = v;
+        s += v;
+    }
+    if (colsum) colsum[(size_t)blk * N + n] = s;
+}
+
+__global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restrict__ ws, int M, int N, int group_rows,
+        const float* __restrict__ scale, const float* __restrict__ shift, float* pooled, int* argidx) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    const int g = blockIdx.y;
+    if (n >= N) return;
+    const int bpg = group_rows / BM;
+    const float sc = scale[n], sh = shift[n];
+    const bool up = sc >= 0.f;    // relu(sc*y+sh) is non-decreasing in y iff sc >= 0
+    float best = up ? -__builtin_inff() : __builtin_inff();
+    int bi = 0x7fffffff;
+    for (int b = g * bpg; b < (g + 1) * bpg && b * BM < M; ++b) {
+        const float* pw = ws + (size_t)b * 4 * N;
+        const float v = up ? pw[n] : pw[2 * N + n];
+        const int vi = reinterpret_cast<const int*>(pw)[(up ? 1 : 3) * N + n];
+        if ((up ? v > best : v < best) || (v == best && vi < bi)) { best = v; bi = vi; }
+    }
+    pooled[(size_t)g * N + n] = fmaxf(__builtin_fmaf(best, sc, sh), 0.f);
+    argidx[(size_t)g * N + n] = bi;
+}
+
+// general max-pool (any group size): per (group, column) scan of the raw layer output
+__global__ __launch_bounds__(256) void pool_rows_kernel(const float* __restrict__ Y, int N, int group_rows,
+        const float* __restrict__ scale, const float* __restrict__ shift, float* pooled, int* argidx) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    const int g = blockIdx.y;
+    if (n >= N) return;
+    const float sc = scale[n], sh = shift[n];
+    const bool up = sc >= 0.f;
+    float best = up ? -__builtin_inff() : __builtin_inff();
+    int bi = g * group_rows;
+    for (int r = g * group_rows; r < (g + 1) * group_rows; ++r) {
+        const float v = Y[(size_t)r * N + n];
+        if (up ? v > best : v < best) { best = v; bi = r; }
+    }
+    pooled[(size_t)g * N + n] = fmaxf(__builtin_fmaf(best, sc, sh), 0.f);
+    argidx[(size_t)g * N + n] = bi;
+}
+
+__global__ __launch_bounds__(256) void group_colsum_kernel(const float* __restrict__ X, int ldx, int N,
+        const int* __restrict__ off, int group_rows, float* __restrict__ out, int ldo) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    const int g = blockIdx.y;
+    if (n >= N) return;
+    const int r0 = off ? off[g] : g * group_rows;
+    const int r1 = off ? off[g + 1] : (g + 1) * group_rows;
+    float s = 0.f;
+    for (int r = r0; r < r1; ++r) s += X[(size_t)r * ldx + n];
+    out[(size_t)g * ldo + n] = s;
+}
+
+template <bool A_KM, bool B_KM, int PA, int PB, int EPI>
+void launch(const UredGemmDesc& d, hipStream_t st) {
+    const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
+    dim3 grid(ntm * ntn, 1, EPI == URED_EPI_SPLITK ? d.splits : 1);
+    hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI>), grid, dim3(NT), 0, st, d);
+}
+
+// The variants the MLP needs: forward (row-major A with prologue, row-major W),
+// dgrad (row-major dY, k-major W), wgrad (k-major dY, k-major activations with prologue).
+int dispatch(const UredGemmDesc& d, hipStream_t st) {
+    const int key = (d.a_kmajor << 12) | (d.b_kmajor << 11) | (d.pro_a << 8) | (d.pro_b << 4) | d.epi;
+#define URED_CASE(AK, BK_, PA, PB, E)                                          \
+    case ((AK << 12) | (BK_ << 11) | (PA << 8) | (PB << 4) | E):              \
+        launch<(bool)AK, (bool)BK_, PA, PB, E>(d, st);                        \
+        return 0;
+    switch (key) {
+        // forward 1x1 conv
+        URED_CASE(0, 0, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_FWD)
+        URED_CASE(0, 0, URED_PRO_ENC, URED_PRO_NONE, URED_EPI_FWD)
+        URED_CASE(0, 0, URED_PRO_RES, URED_PRO_NONE, URED_EPI_FWD)
+        URED_CASE(0, 0, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_STORE)
+        URED_CASE(0, 0, URED_PRO_ENC, URED_PRO_NONE, URED_EPI_STORE)
+        URED_CASE(0, 0, URED_PRO_RES, URED_PRO_NONE, URED_EPI_STORE)
+        // dgrad
+        URED_CASE(0, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_BNBWD)
+        URED_CASE(0, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_STORE)
+        // wgrad (split-K over points)
+        URED_CASE(1, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_SPLITK)
+        URED_CASE(1, 1, URED_PRO_NONE, URED_PRO_ENC, URED_EPI_SPLITK)
+        URED_CASE(1, 1, URED_PRO_NONE, URED_PRO_RES, URED_EPI_SPLITK)
+        default:
+            return ured::set_error(URED_EINVAL, "ured_gemm: unsupported variant a_kmajor=%d b_kmajor=%d pro_a=%d pro_b=%d epi=%d",
+                                   d.a_kmajor, d.b_kmajor, d.pro_a, d.pro_b, d.epi);
+    }
+#undef URED_CASE
+}
+
+}  // namespace
+
+extern "C" {
+
+int ured_gemm(const UredGemmDesc* dp, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(dp, "ured_gemm: null descriptor");
+    const UredGemmDesc& d = *dp;
+    URED_REQUIRE(d.M >= 0 && d.N >= 0 && d.K >= 0, "ured_gemm: negative size");
+    if (d.M == 0 || d.N == 0) return 0;
+    URED_REQUIRE(d.A && d.B && d.C, "ured_gemm: null operand");
+    URED_REQUIRE(d.k1 >= 0 && d.k1 <= d.K, "ured_gemm: k1 %d outside [0,K=%d]", d.k1, d.K);
+    URED_REQUIRE(d.k1 == d.K || (!d.a_kmajor && d.A2), "ured_gemm: A2 split needs row-major A and A2");
+    URED_REQUIRE(d.pro_a == URED_PRO_NONE || (d.pro_s && d.pro_t && !d.a_kmajor), "ured_gemm: bad A prologue");
+    URED_REQUIRE(d.pro_b == URED_PRO_NONE || (d.pro_s && d.pro_t && d.b_kmajor), "ured_gemm: bad B prologue");
+    URED_REQUIRE(!(d.pro_a && d.pro_b), "ured_gemm: one prologue per call");
+    const long long tiles = (long long)((d.M + BM - 1) / BM) * ((d.N + BN - 1) / BN);
+    URED_REQUIRE(tiles < (1LL << 31), "ured_gemm: too many tiles");
+    if (d.epi == URED_EPI_FWD) {
+        URED_REQUIRE(d.stat_ws, "ured_gemm: EPI_FWD needs stat_ws");
+        URED_REQUIRE(!d.rowbias || d.gidx || d.group_rows > 0, "ured_gemm: rowbias needs gidx or group_rows");
+        URED_REQUIRE(!d.pool_ws || (d.group_rows > 0 && d.group_rows % BM == 0),
+                     "ured_gemm: pooling needs group_rows multiple of %d (got %d)", BM, d.group_rows);
+    }
+    if (d.epi == URED_EPI_BNBWD) {
+        URED_REQUIRE(d.Yp && d.bn_mean && d.bn_invstd && d.bn_scale && d.bn_shift && d.bwd_ws, "ured_gemm: EPI_BNBWD inputs");
+        URED_REQUIRE(!d.pool_idx || (d.pool_grad && d.pool_group_rows > 0), "ured_gemm: pool backward needs pool_grad, group rows");
+    }
+    if (d.epi == URED_EPI_SPLITK) URED_REQUIRE(d.splits >= 1 && d.splits <= 65535, "ured_gemm: splits %d", d.splits);
+    int rc = dispatch(d, (hipStream_t)stream);
+    if (rc) return rc;
+    return ured::launch_status("ured_gemm");
+}
+
+int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, int ldo, int accumulate, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(splits >= 1 && M >= 0 && N >= 0 && ldo >= N, "ured_splitk_reduce: bad sizes");
+    if (M == 0 || N == 0) return 0;
+    URED_REQUIRE(ws && out, "ured_splitk_reduce: null pointer");
+    const size_t total = (size_t)M * N;
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ws, splits, M, N, out, ldo, accumulate);
+    return ured::launch_status("ured_splitk_reduce");
+}
+
+int ured_bn_fwd_finalize(const float* stat_ws, int M, int N, const float* gamma, const float* beta,
+                         float eps, float momentum, float* running_mean, float* running_var,
+                         float* mean, float* invstd, float* scale, float* shift, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(M > 0 && N >= 0, "ured_bn_fwd_finalize: bad sizes M=%d N=%d", M, N);
+    if (N == 0) return 0;
+    URED_REQUIRE(stat_ws && mean && invstd && scale && shift, "ured_bn_fwd_finalize: null pointer");
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, stat_ws, M, N, gamma, beta,
+                       eps, momentum, running_mean, running_var, mean, invstd, scale, shift);
+    return ured::launch_status("ured_bn_fwd_finalize");
+}
+
+int ured_bn_bwd_finalize(const float* bwd_ws, int M, int N, const float* gamma, const float* invstd,
+                         float* dgamma, float* dbeta, int accumulate,
+                         float* coef_a, float* coef_b, float* coef_c, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(M > 0 && N >= 0, "ured_bn_bwd_finalize: bad sizes");
+    if (N == 0) return 0;
+    URED_REQUIRE(bwd_ws && invstd && coef_a && coef_b && coef_c, "ured_bn_bwd_finalize: null pointer");
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, bwd_ws, M, N, gamma, invstd,
+                       dgamma, dbeta, accumulate, coef_a, coef_b, coef_c);
+    return ured::launch_status("ured_bn_bwd_finalize");
+}
+
+int ured_bn_bwd_apply(const float* G, const float* Y, int M, int N, int ld, int res,
+                      const float* mean, const float* coef_a, const float* coef_b, const float* coef_c,
+                      float* dY, float* colsum_ws, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(M >= 0 && N >= 0 && ld >= N, "ured_bn_bwd_apply: bad sizes");
+    if (M == 0 || N == 0) return 0;
+    URED_REQUIRE(G && Y && mean && coef_a && coef_b && coef_c && dY, "ured_bn_bwd_apply: null pointer");
+    dim3 grid((N + 255) / 256, (M + BM - 1) / BM);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(256), 0, (hipStream_t)stream, G, Y, M, N, ld, res, mean,
+                       coef_a, coef_b, coef_c, dY, colsum_ws);
+    return ured::launch_status("ured_bn_bwd_apply");
+}
+
+int ured_pool_finalize(const float* pool_ws, int M, int N, int group_rows, const float* scale,
+                       const float* shift, float* pooled, int* argidx, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(M > 0 && N > 0 && group_rows > 0 && group_rows % BM == 0 && M % group_rows == 0,
+                 "ured_pool_finalize: M=%d must be a multiple of group_rows=%d (multiple of %d)", M, group_rows, BM);
+    URED_REQUIRE(pool_ws && scale && shift && pooled && argidx, "ured_pool_finalize: null pointer");
+    dim3 grid((N + 255) / 256, M / group_rows);
+    hipLaunchKernelGGL(pool_finalize_kernel, grid, dim3(256), 0, (hipStream_t)stream, pool_ws, M, N, group_rows,
+                       scale, shift, pooled, argidx);
+    return ured::launch_status("ured_pool_finalize");
+}
+
+int ured_pool_rows(const float* Y, int M, int N, int group_rows, const float* scale, const float* shift,
+                   float* pooled, int* argidx, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(M > 0 && N > 0 && group_rows > 0 && M % group_rows == 0, "ured_pool_rows: bad sizes M=%d group_rows=%d", M, group_rows);
+    URED_REQUIRE(M / group_rows <= 65535, "ured_pool_rows: too many groups");
+    URED_REQUIRE(Y && scale && shift && pooled && argidx, "ured_pool_rows: null pointer");
+    dim3 grid((N + 255) / 256, M / group_rows);
+    hipLaunchKernelGGL(pool_rows_kernel, grid, dim3(256), 0, (hipStream_t)stream, Y, N, group_rows, scale, shift, pooled, argidx);
+    return ured::launch_status("ured_pool_rows");
+}
+
+int ured_group_colsum(const float* X, int ldx, int N, const int* off, int group_rows, int G,
+                      float* out, int ldo, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(N >= 0 && G >= 0 && ldx >= N && ldo >= N, "ured_group_colsum: bad sizes");
+    if (N == 0 || G == 0) return 0;
+    URED_REQUIRE(X && out && (off || group_rows > 0), "ured_group_colsum: null pointer / no grouping");
+    URED_REQUIRE(G <= 65535, "ured_group_colsum: G=%d > 65535", G);
+    dim3 grid((N + 255) / 256, G);
+    hipLaunchKernelGGL(group_colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, ldx, N, off, group_rows, out, ldo);
+    return ured::launch_status("ured_group_colsum");
+}
+
+}  // extern "C"

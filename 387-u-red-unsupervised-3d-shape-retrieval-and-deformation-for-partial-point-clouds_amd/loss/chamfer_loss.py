@@ -1,0 +1,92 @@
+"""Drop-in for the reference loss/chamfer_loss.py (chamfer_distance2, compute_cm_loss).
+
+The reference calls the un-vendored Shape_Measure.distance.ChamferLoss once per
+sample and once per part inside Python loops, with a .item() host sync
+(loss/chamfer_loss.py:5-30). Here every family of calls is ONE ragged HIP
+launch (ured_nn_seg_fwd) with segment tables built on the device:
+  full family : out[b, :k_b*1024]  <->  x[b]
+  part family : out[b, i*1024:(i+1)*1024]  <->  points of part i of x[b]
+ChamferLoss semantics (Shape_Measure is absent, version unpinned): cost1/cost2
+are the squared nearest-neighbour distances, as chamfer_3DDist returns them.
+"""
+import torch
+
+from ured_hip.nn import nn_dense, nn_segments
+from ured_hip.ops import PartBatch, build_parts, segment_sum
+
+NP_PER_PART = 1024
+
+
+class ChamferLoss(torch.nn.Module):
+    """Shape_Measure.distance.ChamferLoss stand-in: (p1 [B,n,3], p2 [B,m,3]) -> (cost1 [B,n], cost2 [B,m])."""
+
+    def forward(self, p1, p2):
+        d1, d2, _, _ = nn_dense(p1, p2)
+        return d1, d2
+
+
+def chamfer_distance2(p1, p2):
+    cost1, cost2 = ChamferLoss()(p1, p2)
+    return cost1.mean(dim=1) + cost2.mean(dim=1)
+
+
+def _as_partbatch(target_p, target_part, mask):
+    """Accept our PartBatch or the reference's list (per sample) of lists (per part) of [n_i,3] tensors."""
+    if isinstance(target_part, PartBatch):
+        return target_part
+    B, N, _ = target_p.shape
+    P = mask.shape[1]
+    xs, labels = [], []
+    for b in range(B):
+        parts = list(target_part[b])
+        xs.append(torch.cat(parts, 0))
+        labels.append(torch.cat([torch.full((p.shape[0],), i, device=target_p.device, dtype=torch.long)
+                                 for i, p in enumerate(parts)]))
+    return build_parts(torch.stack(labels), torch.stack(xs), P)
+
+
+def _full_segments(B, S, N, k, dev, np_per_part):
+    ar = torch.arange(B, device=dev)
+    return torch.stack([ar * S, k * np_per_part, ar * N, torch.full_like(ar, N)], 1).int()
+
+
+def compute_cm_loss(source_p, target_p, target_part=None, mask=None, batch_reduction="mean",
+                    np_per_part=NP_PER_PART):
+    """Returns (mean_b full CD, mean_b part CD) with a mask, else chamfer_distance2 per sample.
+
+    Like the reference, target_part is used only with a mask; CD = mean(cost1) + mean(cost2).
+    """
+    if mask is None:
+        return chamfer_distance2(source_p, target_p)
+    B, S, _ = source_p.shape
+    N = target_p.shape[1]
+    P = mask.shape[1]
+    dev = source_p.device
+    parts = _as_partbatch(target_p, target_part, mask)
+    k = mask.sum(1).round().long()
+    src = source_p.contiguous()
+    # full family
+    segs = _full_segments(B, S, N, k, dev, np_per_part)
+    da, _, db, _ = nn_segments(src, target_p.contiguous(), segs, S, N, 3)
+    n_valid = (k * np_per_part).clamp(min=1).float()
+    full = da.view(B, S).sum(1) / n_valid + db.view(B, N).mean(1)
+    full = torch.where(k > 0, full, torch.full_like(full, float("nan")))
+    # part family: part slot i of sample b <-> points of its i-th part (sorted by label)
+    slot = torch.arange(P, device=dev)
+    valid = slot.unsqueeze(0) < k.unsqueeze(1)
+    a_off = (torch.arange(B, device=dev) * S).unsqueeze(1) + slot.unsqueeze(0) * np_per_part
+    a_len = torch.where(valid, torch.full_like(a_off, np_per_part), torch.zeros_like(a_off))
+    b_off = parts.off[:-1].view(B, P).long()
+    b_len = torch.where(valid, parts.counts, torch.zeros_like(parts.counts))
+    psegs = torch.stack([a_off, a_len, b_off, b_len], -1).view(B * P, 4).int()
+    pa, _, pb, _ = nn_segments(src, parts.x_sorted.contiguous(), psegs, np_per_part, N, 3)
+    nchunk = min(S, P * np_per_part) // np_per_part
+    cost1 = pa.view(B, S)[:, :nchunk * np_per_part].reshape(B, nchunk, np_per_part).mean(-1)
+    if nchunk < P:
+        cost1 = torch.cat([cost1, cost1.new_zeros(B, P - nchunk)], 1)
+    cost2 = segment_sum(pb.view(-1, 1), parts.off, parts.gid).view(B, P) / parts.counts.clamp(min=1).float()
+    part_cd = (cost1 + cost2) * valid.float()
+    part = part_cd.sum(1) / k.float()
+    if batch_reduction == "mean":
+        return full.mean(), part.mean()
+    return full, part

@@ -1,0 +1,56 @@
+"""Drop-in for the reference loss/contrast_loss.py (InfoNCE between target part features and
+source part codes; contrast_loss.py:35-102).
+
+Data-parallel semantics: with a process group the source codes are gathered from
+every rank. The reference's dist.all_gather is not autograd-aware (the gathered
+copies carry no gradient, contrast_loss.py:35-58); that is the default here too.
+differentiable=True keeps this rank's own slice in the graph instead.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+
+def is_dist_avail_and_initialized():
+    return dist.is_available() and dist.is_initialized()
+
+
+def get_world_size():
+    return dist.get_world_size() if is_dist_avail_and_initialized() else 1
+
+
+def get_rank():
+    return dist.get_rank() if is_dist_avail_and_initialized() else 0
+
+
+def all_gather_batch(tensors, differentiable=False):
+    world = get_world_size()
+    if world == 1:
+        return tensors
+    out = []
+    for t in tensors:
+        bufs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(bufs, t.contiguous())
+        if differentiable:
+            bufs[get_rank()] = t
+        out.append(torch.cat(bufs, 0))
+    return out
+
+
+LOGIT_SCALE = math.log(1 / 0.07)
+
+
+def compute_contrast_loss_loss(tgt_part_f, src_f, src_labels, differentiable_gather=False):
+    bs, num_part = src_f.shape[0], src_f.shape[1]
+    t = tgt_part_f.reshape(bs * num_part, -1)
+    s = src_f.reshape(bs * num_part, -1)
+    n = bs * num_part
+    labels = n * get_rank() + torch.arange(n, device=t.device)
+    labels = torch.where(src_labels.reshape(n).to(t.device) == -1, torch.full_like(labels, -1), labels)
+    t_e = F.normalize(t, dim=-1, p=2)
+    s_e = F.normalize(s, dim=-1, p=2)
+    _, s_all = all_gather_batch([t_e, s_e], differentiable=differentiable_gather)
+    scale = torch.tensor(LOGIT_SCALE, device=t.device).exp()
+    return F.cross_entropy(scale * t_e @ s_all.t(), labels, ignore_index=-1)

@@ -1,0 +1,8 @@
+"""ured_hip — the MI355X (gfx950) hot path of U-RED on libured_hip.so.
+
+  _lib     ctypes loader of the C-ABI (include/ured_hip.h); raises if missing
+  nn       nearest-neighbour / chamfer autograd ops (dense + ragged segments)
+  kernels  typed wrappers of the fused per-point MLP entry points
+  mlp      PointEncoderFn / ResidualNetFn autograd chains
+"""
+from . import _lib, kernels, nn  # noqa: F401

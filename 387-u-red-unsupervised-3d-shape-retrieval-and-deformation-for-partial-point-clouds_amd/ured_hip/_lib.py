@@ -58,6 +58,16 @@ def lib():
     return _lib
 
 
+def register(sigs):
+    """Add entry points (name -> argtypes); applied now if the library is loaded."""
+    _SIGNATURES.update(sigs)
+    if _lib is not None:
+        for name, argtypes in sigs.items():
+            fn = getattr(_lib, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+
+
 def exported_symbols():
     return ["ured_abi_version", "ured_last_error"] + list(_SIGNATURES)
 

@@ -1,0 +1,184 @@
+"""Thin typed wrappers over the MLP entry points of libured_hip.so (no autograd).
+
+Every wrapper launches on torch's current stream of the output's device and
+raises on a non-zero status. Activations are point-major [M][C] fp32 tensors.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+PRO_NONE, PRO_ENC, PRO_RES = 0, 1, 2
+EPI_STORE, EPI_FWD, EPI_BNBWD, EPI_SPLITK = 0, 1, 2, 3
+BM = 128
+
+_P, _I = ctypes.c_void_p, ctypes.c_int
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [("M", _I), ("N", _I), ("K", _I),
+                ("a_kmajor", _I), ("b_kmajor", _I), ("pro_a", _I), ("pro_b", _I), ("epi", _I),
+                ("A", _P), ("lda", _I), ("A2", _P), ("lda2", _I), ("k1", _I),
+                ("B", _P), ("ldb", _I), ("pro_s", _P), ("pro_t", _P),
+                ("C", _P), ("ldc", _I), ("bias", _P), ("rowbias", _P), ("ldr", _I),
+                ("gidx", _P), ("group_rows", _I), ("stat_relu", _I), ("stat_ws", _P), ("pool_ws", _P),
+                ("Yp", _P), ("ldy", _I), ("bn_mean", _P), ("bn_invstd", _P), ("bn_scale", _P), ("bn_shift", _P),
+                ("bwd_res", _I), ("pool_idx", _P), ("pool_grad", _P), ("pool_group_rows", _I),
+                ("bwd_ws", _P), ("splits", _I)]
+
+
+_SIGS = {
+    "ured_gemm": [ctypes.POINTER(GemmDesc), _P],
+    "ured_splitk_reduce": [_P, _I, _I, _I, _P, _I, _I, _P],
+    "ured_bn_fwd_finalize": [_P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P],
+    "ured_bn_bwd_finalize": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P],
+    "ured_bn_bwd_apply": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "ured_pool_finalize": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
+    "ured_group_colsum": [_P, _I, _I, _P, _I, _I, _P, _I, _P],
+    "ured_pool_rows": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
+}
+_lib.register(_SIGS)
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _addr(t, elem_offset=0):
+    return None if t is None else t.data_ptr() + 4 * elem_offset
+
+
+def nblocks(M):
+    return (M + BM - 1) // BM
+
+
+def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro_a=PRO_NONE, pro_b=PRO_NONE,
+         epi=EPI_STORE, A_off=0, B_off=0, C_off=0, A2=None, lda2=0, k1=None, pro_s=None, pro_t=None, bias=None,
+         rowbias=None, ldr=0, gidx=None, group_rows=0, stat_relu=False, stat_ws=None, pool_ws=None,
+         Yp=None, ldy=0, bn=None, bwd_res=False, pool_idx=None, pool_grad=None, pool_group_rows=0,
+         bwd_ws=None, splits=1):
+    """One ured_gemm launch. Offsets are in elements of the respective tensor."""
+    d = GemmDesc()
+    d.M, d.N, d.K = int(M), int(N), int(K)
+    d.a_kmajor, d.b_kmajor, d.pro_a, d.pro_b, d.epi = int(a_kmajor), int(b_kmajor), pro_a, pro_b, epi
+    d.A, d.lda = _addr(A, A_off), int(lda)
+    d.A2, d.lda2, d.k1 = _p(A2), int(lda2), int(K if k1 is None else k1)
+    d.B, d.ldb = _addr(B, B_off), int(ldb)
+    d.pro_s, d.pro_t = _p(pro_s), _p(pro_t)
+    d.C, d.ldc = _addr(C, C_off), int(ldc)
+    d.bias, d.rowbias, d.ldr = _p(bias), _p(rowbias), int(ldr)
+    d.gidx, d.group_rows, d.stat_relu = _p(gidx), int(group_rows), int(bool(stat_relu))
+    d.stat_ws, d.pool_ws = _p(stat_ws), _p(pool_ws)
+    d.Yp, d.ldy = _p(Yp), int(ldy)
+    if bn is not None:
+        d.bn_mean, d.bn_invstd, d.bn_scale, d.bn_shift = _p(bn.mean), _p(bn.invstd), _p(bn.scale), _p(bn.shift)
+    d.bwd_res = int(bool(bwd_res))
+    d.pool_idx, d.pool_grad, d.pool_group_rows = _p(pool_idx), _p(pool_grad), int(pool_group_rows)
+    d.bwd_ws, d.splits = _p(bwd_ws), int(splits)
+    _lib.call("ured_gemm", ctypes.byref(d), _lib.stream_of(C))
+
+
+class BNState:
+    """Per-layer batch statistics of a forward pass (device vectors [N])."""
+    __slots__ = ("mean", "invstd", "scale", "shift")
+
+    def __init__(self, mean, invstd, scale, shift):
+        self.mean, self.invstd, self.scale, self.shift = mean, invstd, scale, shift
+
+
+def bn_fwd_finalize(stat_ws, M, N, gamma, beta, eps, momentum, running_mean, running_var):
+    dev = stat_ws.device
+    mean = torch.empty(N, device=dev)
+    invstd = torch.empty(N, device=dev)
+    scale = torch.empty(N, device=dev)
+    shift = torch.empty(N, device=dev)
+    _lib.call("ured_bn_fwd_finalize", _p(stat_ws), int(M), int(N), _p(gamma), _p(beta), float(eps), float(momentum),
+              _p(running_mean), _p(running_var), _p(mean), _p(invstd), _p(scale), _p(shift), _lib.stream_of(stat_ws))
+    return BNState(mean, invstd, scale, shift)
+
+
+def bn_eval_state(gamma, beta, running_mean, running_var, eps):
+    invstd = torch.rsqrt(running_var + eps)
+    scale = gamma * invstd
+    return BNState(running_mean.clone(), invstd, scale, beta - running_mean * scale)
+
+
+def bn_bwd_finalize(bwd_ws, M, N, gamma, invstd, dgamma, dbeta):
+    dev = bwd_ws.device
+    ca, cb, cc = (torch.empty(N, device=dev) for _ in range(3))
+    _lib.call("ured_bn_bwd_finalize", _p(bwd_ws), int(M), int(N), _p(gamma), _p(invstd), _p(dgamma), _p(dbeta), 0,
+              _p(ca), _p(cb), _p(cc), _lib.stream_of(bwd_ws))
+    return ca, cb, cc
+
+
+def bn_bwd_apply(G, Y, res, mean, coefs, want_colsum=True):
+    M, N = Y.shape
+    dY = torch.empty_like(Y)
+    cs = torch.empty(nblocks(M), N, device=Y.device) if want_colsum else None
+    _lib.call("ured_bn_bwd_apply", _p(G), _p(Y), int(M), int(N), int(N), int(bool(res)), _p(mean),
+              _p(coefs[0]), _p(coefs[1]), _p(coefs[2]), _p(dY), _p(cs), _lib.stream_of(Y))
+    return dY, cs
+
+
+def pool_finalize(pool_ws, M, N, group_rows, scale, shift):
+    G = M // group_rows
+    pooled = torch.empty(G, N, device=pool_ws.device)
+    argidx = torch.empty(G, N, device=pool_ws.device, dtype=torch.int32)
+    _lib.call("ured_pool_finalize", _p(pool_ws), int(M), int(N), int(group_rows), _p(scale), _p(shift),
+              _p(pooled), _p(argidx), _lib.stream_of(pool_ws))
+    return pooled, argidx
+
+
+def pool_rows(Y, group_rows, scale, shift):
+    M, N = Y.shape
+    G = M // group_rows
+    pooled = torch.empty(G, N, device=Y.device)
+    argidx = torch.empty(G, N, device=Y.device, dtype=torch.int32)
+    _lib.call("ured_pool_rows", _p(Y), int(M), int(N), int(group_rows), _p(scale), _p(shift), _p(pooled),
+              _p(argidx), _lib.stream_of(Y))
+    return pooled, argidx
+
+
+def group_colsum(X, N, G, *, off=None, group_rows=0, ldx=None, out=None):
+    out = torch.empty(G, N, device=X.device) if out is None else out
+    _lib.call("ured_group_colsum", _p(X), int(N if ldx is None else ldx), int(N), _p(off), int(group_rows), int(G),
+              _p(out), int(out.stride(0)), _lib.stream_of(X))
+    return out
+
+
+def colsum(X):
+    """Column sums of a [R][N] tensor, deterministic two-level (chunks of 1024 rows)."""
+    R, N = X.shape
+    if R <= 4096:
+        return group_colsum(X, N, 1, group_rows=R)[0]
+    nch = (R + 1023) // 1024
+    off = torch.arange(0, nch + 1, device=X.device, dtype=torch.int32) * 1024
+    off[-1] = R
+    part = group_colsum(X, N, nch, off=off)
+    return group_colsum(part, N, 1, group_rows=nch)[0]
+
+
+def splitk_reduce(ws, splits, M, N, out, ldo, accumulate=False, out_off=0):
+    _lib.call("ured_splitk_reduce", _p(ws), int(splits), int(M), int(N), _addr(out, out_off), int(ldo),
+              int(bool(accumulate)), _lib.stream_of(out))
+
+
+def choose_splits(Mo, No, K):
+    tiles = ((Mo + 127) // 128) * ((No + 127) // 128)
+    s = max(1, min(1024 // max(tiles, 1), K // 512))
+    return max(1, min(s, 256))
+
+
+def wgrad(dY, ldd, X, ldx, Cout, Kin, Mrows, out, ldo, *, out_off=0, X_off=0, pro=PRO_NONE, pro_s=None,
+          pro_t=None, accumulate=False):
+    """out[cout][kin] (+)= sum_m dY[m][cout] * pro(X[m][kin]) (split-K over the Mrows points)."""
+    splits = choose_splits(Cout, Kin, Mrows)
+    if splits == 1 and not accumulate:
+        gemm(Cout, Kin, Mrows, dY, ldd, X, ldx, out, ldo, a_kmajor=True, b_kmajor=True, pro_b=pro,
+             pro_s=pro_s, pro_t=pro_t, epi=EPI_SPLITK, splits=1, B_off=X_off, C_off=out_off)
+        return
+    ws = torch.empty(splits, Cout, Kin, device=dY.device)
+    gemm(Cout, Kin, Mrows, dY, ldd, X, ldx, ws, Kin, a_kmajor=True, b_kmajor=True, pro_b=pro,
+         pro_s=pro_s, pro_t=pro_t, epi=EPI_SPLITK, splits=splits, B_off=X_off)
+    splitk_reduce(ws, splits, Cout, Kin, out, ldo, accumulate, out_off)

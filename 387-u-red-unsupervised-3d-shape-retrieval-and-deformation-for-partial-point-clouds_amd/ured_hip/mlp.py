@@ -1,0 +1,298 @@
+"""Fused per-point MLP chains on libured_hip.so, as torch autograd Functions.
+
+PointEncoderFn : TargetEncoder.forward (network/simple_encoder.py:88-107) —
+                 conv 3->64->64 (mlp1), 64->64->128->1024 (mlp2), fuse_sem
+                 (1024+S)->1024, per_point_out 1024->C->C, max-pool + fc —
+                 every Conv1d+BatchNorm1d(train)+ReLU fused into ured_gemm
+                 launches (prologue = previous BN+ReLU, epilogue = stats / pool).
+ResidualNetFn  : re_residual_net.forward (network/deformation_net.py:96-107) with
+                 FeedForwardNet_norm [in,256,256,32,3] (Conv->ReLU->BN), whose
+                 input is cat(per-point features, per-group code): the group half
+                 is folded into a per-group row bias (W_code @ code), so it is
+                 never broadcast to every point.
+Both run forward and backward entirely on HIP kernels; only the tiny
+per-call index bookkeeping is Python.
+"""
+import torch
+from torch.autograd import Function
+
+from . import kernels as K
+
+BN_EPS = 1e-5
+
+
+class EncoderSpec:
+    """Static description of one TargetEncoder call.
+
+    mode "src": x [G*group_rows, 3] with per-group semantics sem [G, S] (row bias)
+    mode "tgt": x [M, 3] with per-point semantics sem [M, S] (extra K columns)
+    bn_modules: the 7 BatchNorm1d modules (running stats updated in place when training)
+    """
+
+    def __init__(self, mode, group_rows, training, bn_modules, momentum=0.1, eps=BN_EPS):
+        assert mode in ("src", "tgt")
+        self.mode, self.group_rows, self.training = mode, group_rows, training
+        self.bn_modules, self.momentum, self.eps = bn_modules, momentum, eps
+
+
+def _bn_state(spec, i, Yws, M, N, gamma, beta):
+    bnm = spec.bn_modules[i]
+    if spec.training:
+        if bnm.num_batches_tracked is not None:
+            bnm.num_batches_tracked.add_(1)
+        mom = bnm.momentum if bnm.momentum is not None else 0.0
+        return K.bn_fwd_finalize(Yws, M, N, gamma, beta, spec.eps, mom, bnm.running_mean, bnm.running_var)
+    return K.bn_eval_state(gamma, beta, bnm.running_mean, bnm.running_var, spec.eps)
+
+
+class PointEncoderFn(Function):
+    """params: W1,b1,g1,be1, ..., W7,b7,g7,be7, W8,b8, fcW, fcb  (32 tensors)."""
+
+    @staticmethod
+    def forward(ctx, spec, x, sem, *params):
+        x = x.contiguous()
+        sem = sem.contiguous()
+        M = x.shape[0]
+        GR = spec.group_rows
+        G = M // GR
+        dev = x.device
+        Ws = [params[4 * i].reshape(params[4 * i].shape[0], -1) for i in range(7)]
+        bs = [params[4 * i + 1] for i in range(7)]
+        gs = [params[4 * i + 2] for i in range(7)]
+        bes = [params[4 * i + 3] for i in range(7)]
+        W8, b8, fcW, fcb = params[28].reshape(params[28].shape[0], -1), params[29], params[30], params[31]
+        Ys, states = [], []
+        h, kin, pro, st = x, 3, K.PRO_NONE, None
+        pool_ws = None
+        for i in range(7):
+            W = Ws[i]
+            N = W.shape[0]
+            Y = torch.empty(M, N, device=dev)
+            sws = torch.empty(K.nblocks(M), 2, N, device=dev)
+            kw = {}
+            if i == 5:   # fuse_sem: (1024 + S) -> 1024, then max-pool over each group
+                if GR % K.BM == 0:   # pooling partials fused into the GEMM epilogue
+                    pool_ws = torch.empty(K.nblocks(M), 4, N, device=dev)
+                    kw.update(pool_ws=pool_ws)
+                kw.update(group_rows=GR)
+                S = sem.shape[1]
+                if spec.mode == "src":
+                    rb = torch.empty(G, N, device=dev)
+                    K.gemm(G, N, S, sem, S, W, W.shape[1], rb, N, B_off=kin)
+                    kw.update(rowbias=rb, ldr=N)
+                    Kdim = kin
+                else:
+                    kw.update(A2=sem, lda2=S, k1=kin)
+                    Kdim = kin + S
+            else:
+                Kdim = kin
+            K.gemm(M, N, Kdim, h, h.shape[1], W, W.shape[1], Y, N, pro_a=pro,
+                   pro_s=None if st is None else st.scale, pro_t=None if st is None else st.shift,
+                   bias=bs[i], epi=K.EPI_FWD, stat_ws=sws, **kw)
+            st = _bn_state(spec, i, sws, M, N, gs[i], bes[i])
+            Ys.append(Y)
+            states.append(st)
+            h, kin, pro = Y, N, K.PRO_ENC
+        C = W8.shape[0]
+        pp = torch.empty(M, C, device=dev)
+        K.gemm(M, C, kin, h, kin, W8, W8.shape[1], pp, C, pro_a=K.PRO_ENC, pro_s=st.scale, pro_t=st.shift, bias=b8)
+        if pool_ws is not None:
+            pooled, argidx = K.pool_finalize(pool_ws, M, Ws[5].shape[0], GR, states[5].scale, states[5].shift)
+        else:
+            pooled, argidx = K.pool_rows(Ys[5], GR, states[5].scale, states[5].shift)
+        code = torch.empty(G, C, device=dev)
+        K.gemm(G, C, pooled.shape[1], pooled, pooled.shape[1], fcW, fcW.shape[1], code, C, bias=fcb)
+        ctx.spec = spec
+        ctx.states = states
+        ctx.save_for_backward(x, sem, pooled, argidx, *Ys, *params)
+        return code, pp
+
+    @staticmethod
+    def backward(ctx, dcode, dpp):
+        spec, states = ctx.spec, ctx.states
+        saved = ctx.saved_tensors
+        x, sem, pooled, argidx = saved[:4]
+        Ys = list(saved[4:11])
+        params = saved[11:]
+        M = x.shape[0]
+        GR = spec.group_rows
+        G = M // GR
+        dev = x.device
+        Ws = [params[4 * i].reshape(params[4 * i].shape[0], -1) for i in range(7)]
+        gs = [params[4 * i + 2] for i in range(7)]
+        W8, fcW = params[28].reshape(params[28].shape[0], -1), params[30]
+        C = W8.shape[0]
+        grads = [None] * 32
+        dcode = torch.zeros(G, C, device=dev) if dcode is None else dcode.contiguous()
+        dpp = torch.zeros(M, C, device=dev) if dpp is None else dpp.contiguous()
+        # fc: code = pooled @ fcW^T + fcb
+        NP = pooled.shape[1]
+        dpool = torch.empty(G, NP, device=dev)
+        K.gemm(G, NP, C, dcode, C, fcW, NP, dpool, NP, b_kmajor=True)
+        dfcW = torch.empty_like(fcW)
+        K.wgrad(dcode, C, pooled, NP, C, NP, G, dfcW, NP)
+        grads[30], grads[31] = dfcW, K.colsum(dcode)
+        # per_point_out.3 (no BN): dW8 = dpp^T @ H7
+        dW8 = torch.empty(W8.shape, device=dev)
+        K.wgrad(dpp, C, Ys[6], Ys[6].shape[1], C, W8.shape[1], M, dW8, W8.shape[1],
+                pro=K.PRO_ENC, pro_s=states[6].scale, pro_t=states[6].shift)
+        grads[28], grads[29] = dW8.view(params[28].shape), K.colsum(dpp)
+        dY, Wn = dpp, W8   # gradient at the output of the layer above, and that layer's weight
+        for i in range(6, -1, -1):
+            Y, st = Ys[i], states[i]
+            N = Y.shape[1]
+            Cn = dY.shape[1]
+            G_ = torch.empty(M, N, device=dev)
+            bws = torch.empty(K.nblocks(M), 2, N, device=dev)
+            kw = {}
+            if i == 5:
+                kw.update(pool_idx=argidx, pool_grad=dpool, pool_group_rows=GR)
+            # dH_i = dY_{i+1} @ W_{i+1}[:, :N]; fused ReLU mask + BN-backward partials of layer i
+            K.gemm(M, N, Cn, dY, Cn, Wn, Wn.shape[1], G_, N, b_kmajor=True, epi=K.EPI_BNBWD,
+                   Yp=Y, ldy=N, bn=st, bwd_res=False, bwd_ws=bws, **kw)
+            dgamma, dbeta = torch.empty(N, device=dev), torch.empty(N, device=dev)
+            coefs = K.bn_bwd_finalize(bws, M, N, gs[i], st.invstd, dgamma, dbeta)
+            dYi, cs = K.bn_bwd_apply(G_, Y, False, st.mean, coefs)
+            W = Ws[i]
+            dW = torch.empty(W.shape, device=dev)
+            if i == 0:
+                K.wgrad(dYi, N, x, 3, N, 3, M, dW, 3)
+            else:
+                Xp, stp = Ys[i - 1], states[i - 1]
+                kin = Xp.shape[1]
+                K.wgrad(dYi, N, Xp, kin, N, kin, M, dW, W.shape[1], pro=K.PRO_ENC, pro_s=stp.scale, pro_t=stp.shift)
+                if i == 5:   # semantic columns of fuse_sem
+                    S = sem.shape[1]
+                    if spec.mode == "src":
+                        D = K.group_colsum(dYi, N, G, group_rows=GR)
+                        K.wgrad(D, N, sem, S, N, S, G, dW, W.shape[1], out_off=kin)
+                    else:
+                        K.wgrad(dYi, N, sem, S, N, S, M, dW, W.shape[1], out_off=kin)
+            grads[4 * i] = dW.view(params[4 * i].shape)
+            grads[4 * i + 1] = K.group_colsum(cs, N, 1, group_rows=cs.shape[0])[0]
+            grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
+            dY, Wn = dYi, W
+        return (None, None, None) + tuple(grads)
+
+
+class ResidualNetFn(Function):
+    """re_residual_net on cat(per-point pp [M,Cp], group code [G,Cc]).
+
+    params: W1,b1,g1,be1, W2,b2,g2,be2, W3,b3,g3,be3, W4,b4 (14 tensors).
+    code_first: True when the input is cat(code, pp) (recon_decoder_src).
+    grouping: gidx int32 [M] (row -> group) + off int32 [G+1], or fixed group_rows.
+    """
+
+    @staticmethod
+    def forward(ctx, spec, pp, code, *params):
+        code_first, gidx, off, group_rows, training, bn_modules = spec
+        pp = pp.contiguous()
+        code = code.contiguous()
+        M, Cp = pp.shape
+        G, Cc = code.shape
+        dev = pp.device
+        W1 = params[0].reshape(params[0].shape[0], -1)
+        ld1 = W1.shape[1]
+        assert ld1 == Cp + Cc
+        pp_off, code_off = (Cc, 0) if code_first else (0, Cp)
+        N1 = W1.shape[0]
+        rb = None
+        if Cc > 0:   # the group half of the concatenated input becomes a per-group row bias
+            rb = torch.empty(G, N1, device=dev)
+            K.gemm(G, N1, Cc, code, Cc, W1, ld1, rb, N1, B_off=code_off)
+        Ys, states = [], []
+        h, kin, pro, st = pp, Cp, K.PRO_NONE, None
+        for i in range(3):
+            W = params[4 * i].reshape(params[4 * i].shape[0], -1)
+            N = W.shape[0]
+            Y = torch.empty(M, N, device=dev)
+            sws = torch.empty(K.nblocks(M), 2, N, device=dev)
+            kw = {}
+            if i == 0:
+                kw = dict(B_off=pp_off)
+                if rb is not None:
+                    kw.update(rowbias=rb, ldr=N1, gidx=gidx, group_rows=group_rows)
+            K.gemm(M, N, kin, h, h.shape[1], W, W.shape[1], Y, N, pro_a=pro,
+                   pro_s=None if st is None else st.scale, pro_t=None if st is None else st.shift,
+                   bias=params[4 * i + 1], epi=K.EPI_FWD, stat_ws=sws, stat_relu=True, **kw)
+            bnm = bn_modules[i]
+            if training:
+                if bnm.num_batches_tracked is not None:
+                    bnm.num_batches_tracked.add_(1)
+                st = K.bn_fwd_finalize(sws, M, N, params[4 * i + 2], params[4 * i + 3], BN_EPS,
+                                       bnm.momentum if bnm.momentum is not None else 0.0,
+                                       bnm.running_mean, bnm.running_var)
+            else:
+                st = K.bn_eval_state(params[4 * i + 2], params[4 * i + 3], bnm.running_mean, bnm.running_var, BN_EPS)
+            Ys.append(Y)
+            states.append(st)
+            h, kin, pro = Y, N, K.PRO_RES
+        W4 = params[12].reshape(params[12].shape[0], -1)
+        out = torch.empty(M, W4.shape[0], device=dev)
+        K.gemm(M, W4.shape[0], kin, h, kin, W4, W4.shape[1], out, W4.shape[0], pro_a=K.PRO_RES,
+               pro_s=st.scale, pro_t=st.shift, bias=params[13])
+        ctx.spec, ctx.states = spec, states
+        ctx.save_for_backward(pp, code, *Ys, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        code_first, gidx, off, group_rows, training, bn_modules = ctx.spec
+        states = ctx.states
+        saved = ctx.saved_tensors
+        pp, code = saved[:2]
+        Ys = list(saved[2:5])
+        params = saved[5:]
+        M, Cp = pp.shape
+        G, Cc = code.shape
+        dev = pp.device
+        grads = [None] * 14
+        dout = dout.contiguous()
+        W4 = params[12].reshape(params[12].shape[0], -1)
+        No = W4.shape[0]
+        dW4 = torch.empty(W4.shape, device=dev)
+        K.wgrad(dout, No, Ys[2], Ys[2].shape[1], No, W4.shape[1], M, dW4, W4.shape[1],
+                pro=K.PRO_RES, pro_s=states[2].scale, pro_t=states[2].shift)
+        grads[12], grads[13] = dW4.view(params[12].shape), K.colsum(dout)
+        dY, Wn = dout, W4
+        W1 = params[0].reshape(params[0].shape[0], -1)
+        ld1 = W1.shape[1]
+        pp_off, code_off = (Cc, 0) if code_first else (0, Cp)
+        for i in range(2, -1, -1):
+            Y, st = Ys[i], states[i]
+            N = Y.shape[1]
+            Cn = dY.shape[1]
+            G_ = torch.empty(M, N, device=dev)
+            bws = torch.empty(K.nblocks(M), 2, N, device=dev)
+            K.gemm(M, N, Cn, dY, Cn, Wn, Wn.shape[1], G_, N, b_kmajor=True, epi=K.EPI_BNBWD,
+                   Yp=Y, ldy=N, bn=st, bwd_res=True, bwd_ws=bws)
+            dgamma, dbeta = torch.empty(N, device=dev), torch.empty(N, device=dev)
+            coefs = K.bn_bwd_finalize(bws, M, N, params[4 * i + 2], st.invstd, dgamma, dbeta)
+            dYi, cs = K.bn_bwd_apply(G_, Y, True, st.mean, coefs)
+            W = params[4 * i].reshape(params[4 * i].shape[0], -1)
+            dW = torch.empty(W.shape, device=dev)
+            if i == 0:
+                K.wgrad(dYi, N, pp, Cp, N, Cp, M, dW, ld1, out_off=pp_off)
+                D = None
+                if Cc > 0:
+                    if off is not None:
+                        D = K.group_colsum(dYi, N, G, off=off)
+                    else:
+                        D = K.group_colsum(dYi, N, G, group_rows=group_rows)
+                    K.wgrad(D, N, code, Cc, N, Cc, G, dW, ld1, out_off=code_off)
+            else:
+                Xp, stp = Ys[i - 1], states[i - 1]
+                K.wgrad(dYi, N, Xp, Xp.shape[1], N, Xp.shape[1], M, dW, W.shape[1],
+                        pro=K.PRO_RES, pro_s=stp.scale, pro_t=stp.shift)
+            grads[4 * i] = dW.view(params[4 * i].shape)
+            grads[4 * i + 1] = K.group_colsum(cs, N, 1, group_rows=cs.shape[0])[0]
+            grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
+            dY, Wn = dYi, W
+        # input gradients: dpp = dY1 @ W1[:, pp cols]; dcode = D @ W1[:, code cols]
+        N1 = W1.shape[0]
+        dpp = torch.empty(M, Cp, device=dev)
+        K.gemm(M, Cp, N1, dY, N1, W1, ld1, dpp, Cp, b_kmajor=True, B_off=pp_off)
+        dcode = torch.zeros(G, Cc, device=dev)
+        if Cc > 0:
+            K.gemm(G, Cc, N1, D, N1, W1, ld1, dcode, Cc, b_kmajor=True, B_off=code_off)
+        return (None, dpp, dcode) + tuple(grads)

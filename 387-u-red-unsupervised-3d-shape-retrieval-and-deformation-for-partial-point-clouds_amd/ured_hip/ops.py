@@ -1,0 +1,91 @@
+"""Small device-side helpers of the U-RED step (segment sums, part bookkeeping).
+
+SegmentSumFn  : rows of x grouped into contiguous segments -> per-segment sums
+                (HIP ured_group_colsum, fixed row order: deterministic).
+PartBatch     : the ragged per-part view of a target batch that the reference
+                builds with Python loops + torch.unique + boolean masks
+                (engine/train.py:103-136): points sorted by part label, part
+                offsets/counts, per-point part id, the mask of present parts.
+build_parts   : computes a PartBatch with device ops only (no host sync).
+"""
+import torch
+from torch.autograd import Function
+
+from . import kernels as K
+
+
+class SegmentSumFn(Function):
+    @staticmethod
+    def forward(ctx, x, off, gid):
+        x = x.contiguous()
+        G = off.shape[0] - 1
+        out = K.group_colsum(x, x.shape[1], G, off=off)
+        ctx.save_for_backward(gid)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (gid,) = ctx.saved_tensors
+        return gout.index_select(0, gid.long()), None, None
+
+
+def segment_sum(x, off, gid):
+    """x [R, C], off int32 [G+1] (row ranges), gid int32 [R] (segment of each row) -> [G, C]."""
+    return SegmentSumFn.apply(x, off, gid)
+
+
+class PartBatch:
+    """Per-part view of a target batch.
+
+    x_sorted [B, N, 3]  points ordered by part label (stable), i.e. the
+                        reference's torch.cat over part_x[b] (engine/train.py:119,133)
+    perm     [B, N]     original index of each sorted point
+    gid      [B*N] i32  global part slot (b*P + rank) of each sorted point
+    off      [B*P+1] i32 row offsets of each part slot in the flattened sorted rows
+    counts   [B, P]     points per part slot (0 for padding slots)
+    k        [B]        number of parts per sample (= mask.sum(1))
+    mask     [B, P]     1 for present part slots (engine/train.py:131)
+    rank_of_label [B, P] slot of each label value (valid where present)
+    present  [B, P]     label value present in the sample
+    """
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def __len__(self):
+        return self.x_sorted.shape[0]
+
+
+def build_parts(labels, x, max_parts):
+    B, N = labels.shape
+    P = max_parts
+    dev = x.device
+    lab = labels.long()
+    counts_lab = torch.zeros(B, P, dtype=torch.int64, device=dev).scatter_add_(1, lab, torch.ones_like(lab))
+    present = counts_lab > 0
+    rank_of_label = torch.cumsum(present.long(), 1) - 1
+    k = present.sum(1)
+    slots = torch.arange(P, device=dev)
+    mask = (slots.unsqueeze(0) < k.unsqueeze(1)).float()
+    lab_sorted, perm = torch.sort(lab, dim=1, stable=True)
+    x_sorted = torch.gather(x, 1, perm.unsqueeze(-1).expand(-1, -1, 3))
+    rank_sorted = torch.gather(rank_of_label, 1, lab_sorted)
+    counts = torch.zeros(B, P, dtype=torch.int64, device=dev).scatter_add_(
+        1, rank_of_label.clamp(min=0), counts_lab * present)
+    starts = torch.cumsum(counts, 1) - counts
+    base = (torch.arange(B, device=dev) * N).unsqueeze(1)
+    off = torch.cat([(base + starts).reshape(-1), torch.full((1,), B * N, device=dev, dtype=torch.int64)]).int()
+    gid = (rank_sorted + (torch.arange(B, device=dev) * P).unsqueeze(1)).reshape(-1).int()
+    return PartBatch(x_sorted=x_sorted, perm=perm, gid=gid, off=off, counts=counts, k=k, mask=mask,
+                     rank_of_label=rank_of_label, present=present, max_parts=P)
+
+
+def part_aabb(parts):
+    """[B, P, 6] = (center, half extent) per part slot (compute_aabbox, dataset_utils.py:77-85)."""
+    B, N, _ = parts.x_sorted.shape
+    P = parts.max_parts
+    idx = parts.gid.long().unsqueeze(1).expand(-1, 3)
+    flat = parts.x_sorted.reshape(-1, 3)
+    lo = torch.zeros(B * P, 3, device=flat.device).scatter_reduce(0, idx, flat, "amin", include_self=False)
+    hi = torch.zeros(B * P, 3, device=flat.device).scatter_reduce(0, idx, flat, "amax", include_self=False)
+    return torch.cat([(lo + hi) / 2.0, (hi - lo) / 2.0], 1).view(B, P, 6)

@@ -77,6 +77,101 @@ int ured_nn_seg_bwd(const float* a, const float* b, const int* segs, int nseg,
                     const float* gd_a, const float* gd_b, const int* idx_a, const int* idx_b,
                     float* ga, float* gb, void* stream);
 
+
+/* ---------------- per-point MLP (1x1 conv) on fp32 MFMA ---------------- *
+ * Replaces the Conv1d(k=1)+BatchNorm1d+ReLU chains of TargetEncoder
+ * (network/simple_encoder.py:52-107) and re_residual_net / FeedForwardNet_norm
+ * (network/deformation_net.py:96-107, attention_graph/attention_utils.py:62-86),
+ * forward and backward, with activations stored point-major [M][C].
+ *
+ * ured_gemm computes C[M][N] = sum_k A'[m][k] B'[k][n] on v_mfma_f32_32x32x2_f32
+ * (exact fp32 fma chains), 128x128x32 tiles, where
+ *   A'[m][k] = a_kmajor ? A[k*lda+m] : (k < k1 ? pro(A[m*lda+k]) : A2[m*lda2+k-k1])
+ *   B'[k][n] = b_kmajor ? pro_b(B[k*ldb+n]) : B[n*ldb+k]
+ *   pro(x)   = PRO_ENC: max(x*s[c]+t[c],0)   (Conv->BN->ReLU; c = channel = contiguous index)
+ *              PRO_RES: max(x,0)*s[c]+t[c]   (Conv->ReLU->BN)
+ * and an epilogue:
+ *   EPI_STORE : C = acc (+bias[n])
+ *   EPI_FWD   : Y = acc + bias[n] + rowbias[grp(m)][n] stored to C; per-128-row block
+ *               column partials {mean, M2} of p (p = Y, or relu(Y) if stat_relu) into
+ *               stat_ws[blk][2][N]; if pool_ws: per block column {max,argmax,min,argmin}
+ *               of Y into pool_ws[blk][4][N] (group_rows multiple of 128)
+ *   EPI_BNBWD : dh = acc (+ pool_grad[g][n] where pool_idx[g][n] == m); with the previous
+ *               layer's (Y, mean, invstd, scale, shift): ENC g = dh*(Y*scale+shift > 0),
+ *               xhat = (Y-mean)*invstd; RES g = dh, xhat = (relu(Y)-mean)*invstd;
+ *               stores g to C and block column partials {sum g, sum g*xhat} to bwd_ws
+ *   EPI_SPLITK: partial sums of the k-range of blockIdx.z stored to C + z*M*ldc
+ */
+#define URED_PRO_NONE 0
+#define URED_PRO_ENC 1
+#define URED_PRO_RES 2
+#define URED_EPI_STORE 0
+#define URED_EPI_FWD 1
+#define URED_EPI_BNBWD 2
+#define URED_EPI_SPLITK 3
+
+typedef struct UredGemmDesc {
+    int M, N, K;
+    int a_kmajor, b_kmajor, pro_a, pro_b, epi;
+    const float* A; int lda;
+    const float* A2; int lda2; int k1;         /* k >= k1 read from A2 (row-major A only); k1 = K if unused */
+    const float* B; int ldb;
+    const float* pro_s; const float* pro_t;     /* prologue per-channel affine */
+    float* C; int ldc;
+    const float* bias;                          /* [N] or NULL */
+    const float* rowbias; int ldr;              /* [G][ldr] or NULL */
+    const int* gidx; int group_rows;            /* row -> group: gidx[m] or m / group_rows */
+    int stat_relu;
+    float* stat_ws;                             /* [ceil(M/128)][2][N] */
+    float* pool_ws;                             /* [ceil(M/128)][4][N] or NULL */
+    const float* Yp; int ldy;                   /* EPI_BNBWD: previous layer's raw output */
+    const float* bn_mean; const float* bn_invstd; const float* bn_scale; const float* bn_shift;
+    int bwd_res;
+    const int* pool_idx; const float* pool_grad; int pool_group_rows;
+    float* bwd_ws;                              /* [ceil(M/128)][2][N] */
+    int splits;                                 /* EPI_SPLITK: gridDim.z (k-range per split = ceil(K/splits/32)*32) */
+} UredGemmDesc;
+
+int ured_gemm(const UredGemmDesc* d, void* stream);
+
+/* Sum split-K partials: out[m][n] = (accumulate ? out : 0) + sum_z ws[z][m][n] (z ascending). */
+int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, int ldo, int accumulate, void* stream);
+
+/* BN forward finalize over the per-block partials of EPI_FWD (M rows, blocks of 128):
+ * fp64 Chan merge -> mean, invstd = 1/sqrt(var_biased+eps), scale = gamma*invstd,
+ * shift = beta - mean*scale; running stats (if non-NULL) updated in place with
+ * momentum and the unbiased variance (torch.nn.BatchNorm1d semantics). */
+int ured_bn_fwd_finalize(const float* stat_ws, int M, int N, const float* gamma, const float* beta,
+                         float eps, float momentum, float* running_mean, float* running_var,
+                         float* mean, float* invstd, float* scale, float* shift, void* stream);
+
+/* BN backward finalize over EPI_BNBWD partials: dbeta = sum g, dgamma = sum g*xhat
+ * (fp64, fixed order; written, or added if accumulate) and the coefficients of
+ * dY = coef_a*g + coef_b*(p - mean) + coef_c (see ured_bn_bwd_apply). */
+int ured_bn_bwd_finalize(const float* bwd_ws, int M, int N, const float* gamma, const float* invstd,
+                         float* dgamma, float* dbeta, int accumulate,
+                         float* coef_a, float* coef_b, float* coef_c, void* stream);
+
+/* dY[m][n] = coef_a*g + coef_b*(p-mean) + coef_c with p = Y (ENC) or relu(Y) (RES, then
+ * times (Y > 0)). Also writes per-128-row column partial sums of dY to colsum_ws[blk][N]. */
+int ured_bn_bwd_apply(const float* G, const float* Y, int M, int N, int ld, int res,
+                      const float* mean, const float* coef_a, const float* coef_b, const float* coef_c,
+                      float* dY, float* colsum_ws, void* stream);
+
+/* Max-pool finalize (TargetEncoder max_pool1d over each group of group_rows points of
+ * relu(scale*Y+shift)): pooled[g][n] and the winning row index argidx[g][n]. */
+int ured_pool_finalize(const float* pool_ws, int M, int N, int group_rows, const float* scale,
+                       const float* shift, float* pooled, int* argidx, void* stream);
+
+/* Same result as EPI_FWD pooling + ured_pool_finalize for any group size (a direct scan of Y [M][N]). */
+int ured_pool_rows(const float* Y, int M, int N, int group_rows, const float* scale, const float* shift,
+                   float* pooled, int* argidx, void* stream);
+
+/* out[g][n] = sum_{m in [off[g], off[g+1])} X[m*ldx+n] (rows ascending); off == NULL means
+ * fixed groups of group_rows rows. G groups. */
+int ured_group_colsum(const float* X, int ldx, int N, const int* off, int group_rows, int G,
+                      float* out, int ldo, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

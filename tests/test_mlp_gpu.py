@@ -1,0 +1,220 @@
+"""Fused per-point MLP (HIP, fp32 MFMA) vs the fp32 torch-CPU oracle.
+
+Tolerances: forward outputs 2e-4 relative to the tensor's max magnitude;
+gradients 2e-3 relative to max magnitude (fp32 sums over up to 10^5 points in
+a different order); BN running statistics 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ured_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def close(got, ref, rel, name=""):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    assert got.shape == ref.shape, (name, got.shape, ref.shape)
+    scale = max(ref.abs().max().item(), 1e-6)
+    err = (got - ref).abs().max().item()
+    assert err <= rel * scale, f"{name}: max err {err:.3e} > {rel:.1e} * {scale:.3e}"
+
+
+@pytest.fixture(scope="module")
+def K(dev):
+    from ured_hip import kernels
+    return kernels
+
+
+@pytest.mark.parametrize("M,N,Kd", [(1000, 70, 33), (128, 128, 32), (300, 3, 32), (257, 64, 3), (4096, 1024, 64)])
+def test_gemm_forward_store(K, dev, M, N, Kd):
+    g = torch.Generator().manual_seed(M + N + Kd)
+    A = torch.randn(M, Kd, generator=g)
+    W = torch.randn(N, Kd, generator=g)
+    b = torch.randn(N, generator=g)
+    C = torch.empty(M, N, device=dev)
+    K.gemm(M, N, Kd, A.to(dev), Kd, W.to(dev), Kd, C, N, bias=b.to(dev))
+    close(C, A @ W.t() + b, 1e-5, "store")
+
+
+@pytest.mark.parametrize("pro", [1, 2])
+def test_gemm_prologue_stats(K, dev, pro):
+    g = torch.Generator().manual_seed(pro)
+    M, N, Kd = 777, 96, 48
+    X = torch.randn(M, Kd, generator=g)
+    s, t = torch.rand(Kd, generator=g) + 0.5, torch.randn(Kd, generator=g)
+    W = torch.randn(N, Kd, generator=g)
+    Xd = X.to(dev)
+    Y = torch.empty(M, N, device=dev)
+    ws = torch.empty(K.nblocks(M), 2, N, device=dev)
+    K.gemm(M, N, Kd, Xd, Kd, W.to(dev), Kd, Y, N, pro_a=pro, pro_s=s.to(dev), pro_t=t.to(dev),
+           epi=K.EPI_FWD, stat_ws=ws, stat_relu=(pro == 2))
+    h = torch.relu(X * s + t) if pro == 1 else torch.relu(X) * s + t
+    ref = h @ W.t()
+    close(Y, ref, 1e-5, "fwd")
+    gam, bet = torch.rand(N, generator=g) + 0.5, torch.randn(N, generator=g)
+    rm, rv = torch.zeros(N, device=dev), torch.ones(N, device=dev)
+    st = K.bn_fwd_finalize(ws, M, N, gam.to(dev), bet.to(dev), 1e-5, 0.1, rm, rv)
+    p = torch.relu(ref) if pro == 2 else ref
+    mu, var = p.double().mean(0), p.double().var(0, unbiased=False)
+    close(st.mean, mu.float(), 1e-5, "mean")
+    close(st.invstd, (1 / torch.sqrt(var + 1e-5)).float(), 1e-5, "invstd")
+    close(rv, (0.9 + 0.1 * p.double().var(0, unbiased=True)).float(), 1e-5, "running_var")
+
+
+def test_gemm_wgrad_and_dgrad(K, dev):
+    g = torch.Generator().manual_seed(5)
+    M, N, Kd = 20000, 200, 72
+    dY = torch.randn(M, N, generator=g)
+    X = torch.randn(M, Kd, generator=g)
+    W = torch.randn(N, Kd, generator=g)
+    dW = torch.empty(N, Kd, device=dev)
+    K.wgrad(dY.to(dev), N, X.to(dev), Kd, N, Kd, M, dW, Kd)
+    close(dW, dY.double().t() @ X.double(), 1e-5, "wgrad")
+    dX = torch.empty(M, Kd, device=dev)
+    K.gemm(M, Kd, N, dY.to(dev), N, W.to(dev), Kd, dX, Kd, b_kmajor=True)
+    close(dX, dY @ W, 1e-5, "dgrad")
+
+
+CFG = {"source_latent_dim": 64, "target_latent_dim": 64, "sem_latent_dim": 16, "MAX_NUM_PARTS": 16}
+
+
+def _mods(dev):
+    from network.simple_encoder import TargetEncoder
+    from network.deformation_net import re_residual_net
+    P = ured_ref.make_params(CFG, seed=3)
+    tgt = TargetEncoder(64, sem_size=16)
+    tgt.load_state_dict(P["target_encoder_full"], strict=True)
+    src = TargetEncoder(64, is_src=True, sem_size=16)
+    src.load_state_dict(P["src_encoder_all"], strict=True)
+    rn = re_residual_net(128)
+    rn.load_state_dict(P["recon_decoder_full"], strict=True)
+    return P, tgt.to(dev).train(), src.to(dev).train(), rn.to(dev).train()
+
+
+BN_FED_BIAS = ("mlp1.0.bias", "mlp1.3.bias", "mlp2.0.bias", "mlp2.3.bias", "mlp2.6.bias", "fuse_sem.0.bias",
+               "per_point_out.0.bias")  # Conv->BN->ReLU only; Conv->ReLU->BN biases are real
+
+
+def check_grad(got, ref, name, sd_grads, rel=3e-3):
+    """Biases that feed a training-mode BatchNorm have an exactly-zero true gradient (BN
+    subtracts the batch mean), so both sides hold only rounding noise: require that noise to be
+    small against the layer's weight gradient instead of comparing noise to noise."""
+    if name in BN_FED_BIAS:
+        wg = sd_grads[name.replace(".bias", ".weight")].abs().max().item()
+        assert got.abs().max().item() <= 1e-3 * max(wg, 1e-6), name
+        return
+    close(got, ref, rel, name + ".grad")
+
+
+def _req(P):
+    for k, v in P.items():
+        if v.dtype.is_floating_point and "running" not in k:
+            v.requires_grad_(True)
+
+
+@pytest.mark.parametrize("n", [256, 96])
+def test_target_encoder_fwd_bwd(dev, n):
+    P, tgt, _, _ = _mods(dev)
+    Pt = P["target_encoder_full"]
+    _req(Pt)
+    g = torch.Generator().manual_seed(n)
+    x = torch.rand(2, n, 3, generator=g) * 2 - 1
+    sem = torch.randn(2, n, 16, generator=g)
+    w1, w2 = torch.randn(2, 64, generator=g), torch.randn(2, 64, n, generator=g)
+    code, pp = tgt(x.to(dev), sem.to(dev))
+    ((code * w1.to(dev)).sum() + (pp * w2.to(dev)).sum()).backward()
+    rc, rpp = ured_ref.target_encoder(Pt, x, sem, False)
+    ((rc * w1).sum() + (rpp * w2).sum()).backward()
+    close(code, rc, 2e-4, "code")
+    close(pp, rpp, 2e-4, "per_point")
+    sd = dict(tgt.named_parameters())
+    for k, v in Pt.items():
+        if k.startswith("stn") or not v.dtype.is_floating_point:
+            continue
+        if "running" in k:
+            close(dict(tgt.named_buffers())[k], v, 1e-4, k)
+        else:
+            check_grad(sd[k].grad, v.grad, k, {n: p.grad for n, p in sd.items()})
+    assert int(tgt.mlp1[1].num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("n", [128, 40])
+def test_source_encoder_fwd_bwd(dev, n):
+    P, _, src, _ = _mods(dev)
+    Ps = P["src_encoder_all"]
+    _req(Ps)
+    g = torch.Generator().manual_seed(n + 1)
+    x = torch.rand(2, 3, n, 3, generator=g) - 0.5
+    sem = torch.randn(2, 3, 16, generator=g)
+    w1, w2 = torch.randn(6, 64, generator=g), torch.randn(6, 64, n, generator=g)
+    code, pp = src(x.to(dev), sem.to(dev))
+    ((code * w1.to(dev)).sum() + (pp * w2.to(dev)).sum()).backward()
+    rc, rpp = ured_ref.target_encoder(Ps, x, sem, True)
+    ((rc * w1).sum() + (rpp * w2).sum()).backward()
+    close(code, rc, 2e-4, "code")
+    close(pp, rpp, 2e-4, "per_point")
+    sd = dict(src.named_parameters())
+    for k, v in Ps.items():
+        if k.startswith("stn") or not v.dtype.is_floating_point or "running" in k:
+            continue
+        check_grad(sd[k].grad, v.grad, k, {n: p.grad for n, p in sd.items()})
+
+
+def test_encoder_eval_mode(dev):
+    P, tgt, _, _ = _mods(dev)
+    Pt = P["target_encoder_full"]
+    g = torch.Generator().manual_seed(9)
+    x = torch.rand(2, 128, 3, generator=g)
+    sem = torch.randn(2, 128, 16, generator=g)
+    with torch.no_grad():
+        tgt(x.to(dev), sem.to(dev))                      # one train step moves the running stats
+        ured_ref.target_encoder(Pt, x, sem, False)
+        tgt.eval()
+        code, pp = tgt(x.to(dev), sem.to(dev))
+        rc, rpp = ured_ref.target_encoder(Pt, x, sem, False, training=False)
+    close(code, rc, 2e-4, "code_eval")
+    close(pp, rpp, 2e-4, "pp_eval")
+
+
+@pytest.mark.parametrize("code_first,ragged", [(False, False), (True, False), (False, True)])
+def test_residual_net_split(dev, code_first, ragged):
+    P, _, _, rn = _mods(dev)
+    Pr = P["recon_decoder_full"]
+    _req(Pr)
+    g = torch.Generator().manual_seed(11)
+    M, G = 600, 5
+    pp = torch.randn(M, 64, generator=g, requires_grad=True)
+    code = torch.randn(G, 64, generator=g, requires_grad=True)
+    if ragged:
+        cuts = torch.tensor([0, 100, 101, 350, 350, 600])
+        gid = torch.repeat_interleave(torch.arange(G), cuts[1:] - cuts[:-1])
+        kw = dict(gidx=gid.int().to(dev), off=cuts.int().to(dev))
+    else:
+        M = 600
+        gid = torch.arange(M) // 120
+        kw = dict(group_rows=120)
+    feat = torch.cat([code[gid], pp], 1) if code_first else torch.cat([pp, code[gid]], 1)
+    ref = ured_ref.residual_net(Pr, feat.unsqueeze(0)).squeeze(0)
+    w = torch.randn(ref.shape, generator=g)
+    (ref * w).sum().backward()
+    ppd = pp.detach().to(dev).requires_grad_(True)
+    cd = code.detach().to(dev).requires_grad_(True)
+    out = rn.forward_split(ppd, cd, code_first=code_first, **kw)
+    (out * w.to(dev)).sum().backward()
+    close(out, ref, 2e-4, "out")
+    close(ppd.grad, pp.grad, 2e-3, "dpp")
+    close(cd.grad, code.grad, 2e-3, "dcode")
+    sd = dict(rn.named_parameters())
+    for k, v in Pr.items():
+        if v.dtype.is_floating_point and "running" not in k:
+            check_grad(sd[k].grad, v.grad, k, {n: p.grad for n, p in sd.items()})
+
+
+def test_residual_net_plain_forward(dev):
+    P, _, _, rn = _mods(dev)
+    g = torch.Generator().manual_seed(12)
+    f = torch.randn(2, 80, 128, generator=g)
+    close(rn(f.to(dev)), ured_ref.residual_net(P["recon_decoder_full"], f), 2e-4, "plain")
