@@ -8,7 +8,7 @@ import torch
 import torch.nn as nn
 
 from . import get_attention_mechanism
-from .attention_utils import FeedForwardNet_norm
+from .attention_utils import FeedForwardNet_norm, conv1x1
 
 
 class MultiheadAttention(nn.Module):
@@ -25,9 +25,10 @@ class MultiheadAttention(nn.Module):
     def forward(self, query, key, value):
         b = query.shape[0]
         split = (b, self.num_heads, self.embed_dim, -1)
-        out, att = self.attention_func(self.in_proj_q(query).view(split), self.in_proj_k(key).view(split),
-                                       self.in_proj_v(value).view(split))
-        return self.out_proj(out.reshape(b, self.num_heads * self.embed_dim, -1)), att
+        out, att = self.attention_func(conv1x1(self.in_proj_q, query).view(split),
+                                       conv1x1(self.in_proj_k, key).view(split),
+                                       conv1x1(self.in_proj_v, value).view(split))
+        return conv1x1(self.out_proj, out.reshape(b, self.num_heads * self.embed_dim, -1)), att
 
 
 class ResidualAttentionMessagePropagation(nn.Module):

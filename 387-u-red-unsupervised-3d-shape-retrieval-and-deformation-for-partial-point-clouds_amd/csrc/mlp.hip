@@ -599,16 +599,23 @@ __global__ __launch_bounds__(256) void pool_rows_kernel(const float* __restrict_
     argidx[(size_t)g * N + n] = bi;
 }
 
+// out[g][n] = sum of rows [r0, r1) of column n. Block = 4 waves x 64 columns; wave w sums
+// rows r0+w, r0+w+4, ... (a wave reads 256 contiguous bytes per row), waves combined in LDS
+// in fixed order: deterministic.
 __global__ __launch_bounds__(256) void group_colsum_kernel(const float* __restrict__ X, int ldx, int N,
         const int* __restrict__ off, int group_rows, float* __restrict__ out, int ldo) {
-    const int n = blockIdx.x * 256 + threadIdx.x;
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int n = blockIdx.x * 64 + lane;
     const int g = blockIdx.y;
-    if (n >= N) return;
     const int r0 = off ? off[g] : g * group_rows;
     const int r1 = off ? off[g + 1] : (g + 1) * group_rows;
     float s = 0.f;
-    for (int r = r0; r < r1; ++r) s += X[(size_t)r * ldx + n];
-    out[(size_t)g * ldo + n] = s;
+    if (n < N)
+        for (int r = r0 + w; r < r1; r += 4) s += X[(size_t)r * ldx + n];
+    part[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && n < N) out[(size_t)g * ldo + n] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
 }
 
 template <bool A_KM, bool B_KM, int PA, int PB, int EPI>
@@ -760,7 +767,7 @@ int ured_group_colsum(const float* X, int ldx, int N, const int* off, int group_
     if (N == 0 || G == 0) return 0;
     URED_REQUIRE(X && out && (off || group_rows > 0), "ured_group_colsum: null pointer / no grouping");
     URED_REQUIRE(G <= 65535, "ured_group_colsum: G=%d > 65535", G);
-    dim3 grid((N + 255) / 256, G);
+    dim3 grid((N + 63) / 64, G);
     hipLaunchKernelGGL(group_colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, ldx, N, off, group_rows, out, ldo);
     return ured::launch_status("ured_group_colsum");
 }

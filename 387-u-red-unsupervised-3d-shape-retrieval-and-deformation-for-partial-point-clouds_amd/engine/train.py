@@ -1,0 +1,277 @@
+"""Drop-in for the reference engine/train.py: U-RED training on the MI355X hot path.
+
+  python engine/train.py [config.json]          (the reference ignores argv and
+                                                  hard-codes config/config_train_test.json,
+                                                  engine/train.py:362-364; argv is honoured here)
+
+One iteration (engine/train.py:196-345) = source/target encoders, part pooling,
+three residual nets, DeformNet, get_shape, the chamfer / contrast / symmetry /
+residual / reconstruction losses, backward, per-module clip_grad_norm_(5.0) and
+Adam. Differences that do not change results:
+  * the per-sample / per-part Python loops (get_part, compute_cm_loss,
+    residual_retrieval_loss) are device-side ragged ops — no host syncs;
+  * the concatenated residual-net inputs are never materialised (row-bias form);
+  * the embedding layer's gradient is not computed: the reference excludes it from
+    the optimizer (train_utils/optimizer_dm.py:83) and never reads it;
+  * per-step scalar logging (which forces .item() host syncs) is optional (cfg["log_every"]).
+Data: cfg["synthetic"] (default) generates SURVEY §8(d) batches; the reference's
+on-disk PartNet/pickle pipeline is out of scope this round.
+"""
+import datetime
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if os.path.dirname(_HERE) not in sys.path:
+    sys.path.insert(0, os.path.dirname(_HERE))
+
+from dataset import synthetic  # noqa: E402
+from dataset.dataset_utils import get_shape, get_source_info, get_source_points, get_symmetric  # noqa: E402
+from loss.basic_consistency_loss import compute_pc_consistency, compute_pc_consistency_weighted  # noqa: E402
+from loss.basic_loss import residual_retrieval_loss  # noqa: E402
+from loss.chamfer_loss import compute_cm_loss  # noqa: E402
+from loss.contrast_loss import compute_contrast_loss_loss  # noqa: E402
+from network.deformation_net import DeformNet_MatchingNet as DM_decoder  # noqa: E402
+from network.deformation_net import re_residual_net  # noqa: E402
+from network.simple_encoder import TargetEncoder as simple_encoder  # noqa: E402
+from train_utils.load_sources import load_sources  # noqa: E402
+from train_utils.optimizer_dm import define_optimizer_dm_re_recon  # noqa: E402
+from ured_hip.ops import build_parts, part_aabb, segment_sum  # noqa: E402
+
+MODULE_NAMES = ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "re_residual_net_full",
+                "src_encoder_all", "recon_decoder_src", "embedding_layer")
+CLIPPED = ("target_encoder_full", "param_decoder_full", "re_residual_net_full", "recon_decoder_full",
+           "recon_decoder_src", "src_encoder_all")           # engine/train.py:339-344 order
+
+
+def get_models(cfg, device=None):
+    """engine/train.py:39-101: the seven modules (+ checkpoint init), Adam and StepLR."""
+    device = device or cfg["device"]
+    m = {
+        "src_encoder_all": simple_encoder(cfg["source_latent_dim"], is_src=True, sem_size=cfg["sem_latent_dim"]),
+        "recon_decoder_src": re_residual_net(cfg["source_latent_dim"] * 2),
+        "target_encoder_full": simple_encoder(cfg["target_latent_dim"], sem_size=cfg["sem_latent_dim"]),
+        "recon_decoder_full": re_residual_net(cfg["target_latent_dim"] * 2),
+        "param_decoder_full": DM_decoder(cfg["source_latent_dim"] * 3, graph_dim=cfg["source_latent_dim"],
+                                         max_num_parts=cfg["MAX_NUM_PARTS"], matching=False),
+        "embedding_layer": nn.Embedding(42, cfg["sem_latent_dim"]),
+        "re_residual_net_full": re_residual_net(cfg["target_latent_dim"] * 2),
+    }
+    if cfg.get("init_dm"):
+        sd = torch.load(cfg["dm_model_path"], map_location="cpu", weights_only=True)
+        for k in ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "src_encoder_all",
+                  "recon_decoder_src", "embedding_layer"):
+            m[k].load_state_dict(sd[k])
+    if cfg.get("init_re"):
+        sd = torch.load(cfg["re_model_path"], map_location="cpu", weights_only=True)
+        m["re_residual_net_full"].load_state_dict(sd["re_residual_net_full"])
+    for v in m.values():
+        v.to(device, dtype=torch.float).train()
+    opt, sched = define_optimizer_dm_re_recon(m["target_encoder_full"], m["param_decoder_full"],
+                                              m["recon_decoder_full"], m["re_residual_net_full"],
+                                              m["src_encoder_all"], m["recon_decoder_src"],
+                                              m["embedding_layer"], cfg)
+    return m, opt, sched
+
+
+class ReInput:
+    """Lazy re_input_codes_full: cat(per-point features sorted by part, part mean) (engine/train.py:125)."""
+
+    def __init__(self, pp_sorted, part_mean, gid, off):
+        self.pp_sorted, self.part_mean, self.gid, self.off = pp_sorted, part_mean, gid, off
+
+
+def get_part(cfg, per_point_full, target_labels, x):
+    """engine/train.py:103-136 without host syncs. per_point_full [B, N, C].
+
+    Returns (target_part_f [B,P,C], None (the unused per-part feature lists), ReInput,
+    mask_part [B,P], PartBatch (the part_x lists), param_def [B,P,6]).
+    """
+    B, N, C = per_point_full.shape
+    P = cfg["MAX_NUM_PARTS"]
+    parts = build_parts(target_labels, x, P)
+    pp_sorted = torch.gather(per_point_full, 1, parts.perm.unsqueeze(-1).expand(-1, -1, C)).reshape(B * N, C)
+    sums = segment_sum(pp_sorted, parts.off, parts.gid)
+    part_mean = sums / parts.counts.reshape(-1, 1).clamp(min=1).float()
+    aabb = part_aabb(parts)                                            # by part slot (rank)
+    param_def = torch.gather(aabb, 1, parts.rank_of_label.clamp(min=0).unsqueeze(-1).expand(-1, -1, 6))
+    param_def = param_def * parts.present.unsqueeze(-1).float()        # indexed by label value (train.py:120)
+    return (part_mean.view(B, P, C), None, ReInput(pp_sorted, part_mean, parts.gid, parts.off),
+            parts.mask, parts, param_def)
+
+
+class TrainStep:
+    """One U-RED iteration on device-resident inputs (no host sync unless logging)."""
+
+    def __init__(self, cfg, db, device=None):
+        self.cfg = cfg
+        self.db = db
+        self.models, self.optimizer, self.scheduler = get_models(cfg, device)
+        self.np_per_part = db.points.shape[1]
+
+    def forward(self, batch, epoch=0):
+        cfg, M = self.cfg, self.models
+        P = cfg["MAX_NUM_PARTS"]
+        x = batch["x"]
+        B, N, _ = x.shape
+        src_labels = batch["src_labels"]
+        mats, _, src_sem_idx = get_source_info(src_labels, self.db)
+        emb = M["embedding_layer"]
+        with torch.no_grad():          # the embedding is not trained (optimizer_dm.py:83)
+            src_sem_f = emb(src_sem_idx)
+            tgt_sem_f = emb(batch["tgt_sem"])
+        src_points = get_source_points(src_labels, self.db)
+        codes, src_pp = M["src_encoder_all"].forward_pointmajor(src_points, src_sem_f)
+        recon_src_p = M["recon_decoder_src"].forward_split(src_pp, codes, code_first=True,
+                                                           group_rows=self.np_per_part).view(B, P, -1, 3)
+        tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
+        target_part_f, _, re_in, mask_part, part_x, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
+        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
+        re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
+                                                         off=re_in.off).view(B, N, 3)
+        codes = codes.view(B, P, -1)
+        params_full = M["param_decoder_full"](tcode, codes, None)
+        out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
+        contrast_labels = torch.where(src_labels >= 0, torch.ones_like(src_labels), src_labels)
+
+        T = {}
+        loss = out.new_zeros(())
+        if cfg["use_chamfer_loss"] > 0.0:
+            T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask_part,
+                                                                   np_per_part=self.np_per_part)
+            loss = loss + T["cd_loss_full"] * cfg["use_chamfer_loss"] + T["cd_loss_part"] * cfg["use_chamfer_part_loss"]
+        if cfg["use_contrast_loss"] > 0.0:
+            T["contrast_loss"] = compute_contrast_loss_loss(target_part_f, codes, contrast_labels,
+                                                            cfg.get("differentiable_gather", False))
+            loss = loss + T["contrast_loss"] * cfg["use_contrast_loss"]
+        if cfg["use_symmetry_loss"] > 0.0:
+            T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(get_symmetric(out), x, part_x, mask_part,
+                                                                           np_per_part=self.np_per_part)
+            loss = loss + T["ref_cd_loss_full"] * cfg["use_symmetry_loss"]
+        if cfg["use_residuals_reg"] > 0.0 and epoch > cfg["init_p_m_loss"]:
+            T["re_reg_loss_full"], T["reg_loss_full"] = residual_retrieval_loss(x, out.detach(), re_res, mask_part,
+                                                                                np_per_part=self.np_per_part)
+            loss = loss + T["re_reg_loss_full"] * cfg["use_residuals_reg"] + T["reg_loss_full"] * cfg["use_residuals_reg"] * 0.01
+        if cfg["use_recon"] > 0.0:
+            T["recon_loss_full"] = compute_pc_consistency(recon_full_p, x)
+            T["recon_loss_src"] = compute_pc_consistency_weighted(recon_src_p, src_points, mask_part)
+            loss = loss + T["recon_loss_full"] * cfg["use_recon"] + T["recon_loss_src"] * cfg["use_recon"]
+        T["all_loss"] = loss
+        T["_out"] = out
+        T["_params"] = params_full
+        return loss, T
+
+    def clip_and_step(self):
+        for name in CLIPPED:
+            torch.nn.utils.clip_grad_norm_(self.models[name].parameters(), 5.0)
+        self.optimizer.step()
+
+    def step(self, batch, epoch=0):
+        self.optimizer.zero_grad(set_to_none=True)
+        loss, T = self.forward(batch, epoch)
+        loss.backward()
+        self.reduce_gradients()
+        self.clip_and_step()
+        return T
+
+    def reduce_gradients(self):
+        """Data-parallel hook (engine/dp.py overrides); single process: nothing to do."""
+
+    def state_dict(self):
+        m = self.models
+        return {"target_encoder_full": m["target_encoder_full"].state_dict(),
+                "param_decoder_full": m["param_decoder_full"].state_dict(),
+                "re_residual_net_full": m["re_residual_net_full"].state_dict(),
+                "recon_decoder_full": m["recon_decoder_full"].state_dict(),
+                "src_encoder_all": m["src_encoder_all"].state_dict(),
+                "recon_decoder_src": m["recon_decoder_src"].state_dict(),
+                "embedding_layer": m["embedding_layer"].state_dict()}
+
+
+def batch_to_device(b, device):
+    return {"x": torch.as_tensor(b["x"]).to(device), "labels": torch.as_tensor(b["labels"]).to(device),
+            "tgt_sem": torch.as_tensor(b["tgt_sem"]).to(device),
+            "src_labels": torch.as_tensor(b["src_labels"]).to(device)}
+
+
+class SyntheticLoader:
+    """Stands in for DataLoader(partnet_dataset) + get_labels (engine/train.py:167-197)."""
+
+    def __init__(self, cfg, num_sources, device, seed=0):
+        self.cfg, self.ns, self.device, self.seed = cfg, num_sources, device, seed
+        self.n = int(cfg.get("iters_per_epoch", 10))
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        for i in range(self.n):
+            b = synthetic.make_batch(self.cfg["batch_size"], self.cfg.get("num_points", 2048), self.ns,
+                                     max_parts=self.cfg["MAX_NUM_PARTS"], parts=self.cfg.get("parts", 4),
+                                     seed=self.seed * 100003 + i)
+            yield batch_to_device(b, self.device)
+
+
+class _ScalarLog:
+    def __init__(self, logdir):
+        try:
+            from tensorboardX import SummaryWriter
+            self.w = SummaryWriter(logdir=logdir)
+            self.f = None
+        except ImportError:
+            self.w = None
+            os.makedirs(logdir, exist_ok=True)
+            self.f = open(os.path.join(logdir, "scalars.jsonl"), "a")
+
+    def add_scalar(self, tag, value, global_step):
+        if self.w is not None:
+            self.w.add_scalar(tag, value, global_step=global_step)
+        else:
+            self.f.write(json.dumps({"tag": tag, "value": value, "step": global_step}) + "\n")
+
+
+def save_model(model, start, epoch, cfg):
+    now = datetime.datetime.now()
+    log = "> {} | Epoch [{:04d}/{:04d}] | duration: {:.1f}s |".format(now.strftime("%c"), epoch, cfg["epochs"],
+                                                                       (now - start).total_seconds())
+    fname = os.path.join(cfg["log_path"], "checkpoint_{:04d}.pth".format(epoch))
+    print("> Saving model to {}...".format(fname))
+    torch.save(model, fname)
+    with open(os.path.join(cfg["log_path"], "train.log"), "a") as fp:
+        fp.write(log + "\n")
+    print(log)
+
+
+def main(cfg):
+    device = cfg["device"]
+    db, _ = load_sources(cfg, device)
+    trainer = TrainStep(cfg, db, device)
+    loader = SyntheticLoader(cfg, db.num_sources, device, seed=int(cfg.get("seed", 0)))
+    writer = _ScalarLog(cfg["log_path"])
+    log_every = int(cfg.get("log_every", 1))
+    for epoch in range(cfg["epochs"]):
+        start = datetime.datetime.now()
+        print(str(start), "training epoch", str(epoch))
+        for i, batch in enumerate(loader):
+            T = trainer.step(batch, epoch)
+            if log_every and i % log_every == 0:
+                for tag, v in T.items():
+                    if not tag.startswith("_") and tag != "ref_cd_loss_part":
+                        writer.add_scalar(tag, float(v.item()), epoch * len(loader) + i)
+        trainer.scheduler.step()
+        if (epoch + 1) % cfg["save_epoch"] == 0:
+            save_model(trainer.state_dict(), start, epoch, cfg)
+    return trainer
+
+
+if __name__ == "__main__":
+    config_path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(_HERE), "config",
+                                                                       "config_train_test.json")
+    config = json.load(open(config_path))
+    os.makedirs(config["log_path"], exist_ok=True)
+    main(config)

@@ -147,16 +147,29 @@ def group_colsum(X, N, G, *, off=None, group_rows=0, ldx=None, out=None):
     return out
 
 
+_OFF_CACHE = {}
+
+
+def _chunk_offsets(R, chunk, device):
+    key = (R, chunk, str(device))
+    off = _OFF_CACHE.get(key)
+    if off is None:
+        nch = (R + chunk - 1) // chunk
+        o = [min(i * chunk, R) for i in range(nch + 1)]
+        off = torch.tensor(o, dtype=torch.int32, device=device)
+        _OFF_CACHE[key] = off
+    return off
+
+
 def colsum(X):
-    """Column sums of a [R][N] tensor, deterministic two-level (chunks of 1024 rows)."""
+    """Column sums of a [R][N] tensor: deterministic two-level reduction (chunks of 64 rows)."""
     R, N = X.shape
-    if R <= 4096:
+    if R <= 256:
         return group_colsum(X, N, 1, group_rows=R)[0]
-    nch = (R + 1023) // 1024
-    off = torch.arange(0, nch + 1, device=X.device, dtype=torch.int32) * 1024
-    off[-1] = R
-    part = group_colsum(X, N, nch, off=off)
-    return group_colsum(part, N, 1, group_rows=nch)[0]
+    chunk = 64
+    off = _chunk_offsets(R, chunk, X.device)
+    part = group_colsum(X, N, off.shape[0] - 1, off=off)
+    return colsum(part)
 
 
 def splitk_reduce(ws, splits, M, N, out, ldo, accumulate=False, out_off=0):

@@ -169,7 +169,7 @@ class PointEncoderFn(Function):
                     else:
                         K.wgrad(dYi, N, sem, S, N, S, M, dW, W.shape[1], out_off=kin)
             grads[4 * i] = dW.view(params[4 * i].shape)
-            grads[4 * i + 1] = K.group_colsum(cs, N, 1, group_rows=cs.shape[0])[0]
+            grads[4 * i + 1] = K.colsum(cs)
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
         return (None, None, None) + tuple(grads)
@@ -285,7 +285,7 @@ class ResidualNetFn(Function):
                 K.wgrad(dYi, N, Xp, Xp.shape[1], N, Xp.shape[1], M, dW, W.shape[1],
                         pro=K.PRO_RES, pro_s=stp.scale, pro_t=stp.shift)
             grads[4 * i] = dW.view(params[4 * i].shape)
-            grads[4 * i + 1] = K.group_colsum(cs, N, 1, group_rows=cs.shape[0])[0]
+            grads[4 * i + 1] = K.colsum(cs)
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
         # input gradients: dpp = dY1 @ W1[:, pp cols]; dcode = D @ W1[:, code cols]

@@ -122,5 +122,5 @@ def nn_dense(xyz1, xyz2):
 def nn_segments(a, b, segs, max_a, max_b, dirs=3):
     """Returns dist_a, idx_a, dist_b, idx_b over the flat buffers (see NNSegFunction)."""
     a_shape, b_shape = a.shape[:-1], b.shape[:-1]
-    da, ia, db, ib = NNSegFunction.apply(a, b, segs, max_a, max_b, dirs)
+    da, ia, db, ib = NNSegFunction.apply(a.reshape(-1, 3), b.reshape(-1, 3), segs, max_a, max_b, dirs)
     return da.view(a_shape), ia.view(a_shape), db.view(b_shape), ib.view(b_shape)

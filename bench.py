@@ -1,0 +1,232 @@
+"""U-RED training-step benchmark on MI355X (BASELINE.json metric, config 2 by default).
+
+  python bench.py [--gpus N --steps K --warmup W]      (N>1: launched by torch.distributed.run)
+
+A step = one full U-RED training iteration (engine/train.py:196-345): source +
+target encoders, part pooling, 3 residual nets, DeformNet, get_shape, chamfer /
+contrast / symmetry / residual / reconstruction losses, backward, 6x clip, Adam —
+on a synthetic chair-shaped batch (bs=16 per GPU, 2048 points, 16 part slots x
+1024 source points, C=512, S=128, 4 parts per target) resident in HBM.
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+ge.add_pkg_path()
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3      # MI355X fp32 (vector = matrix) dense peak, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def workload_cfg(args):
+    with open(os.path.join(ge.PKG_DIR, "config", "config_train_test.json")) as f:
+        cfg = json.load(f)
+    cfg.update({"batch_size": args.batch, "num_points": args.points, "parts": args.parts,
+                "num_source": args.sources, "device": "cuda", "log_every": 0})
+    return cfg
+
+
+class GemmTimer:
+    """Event pairs around every ured_gemm launch of one extra (untimed-region) step."""
+
+    def __init__(self):
+        self.rec = []
+
+    def __enter__(self):
+        from ured_hip import kernels
+        self.k = kernels
+        self.orig = kernels.gemm
+        rec = self.rec
+
+        def timed(M, N, K, *a, **kw):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.orig(M, N, K, *a, **kw)
+            e1.record()
+            rec.append((kw.get("epi", 0), kw.get("a_kmajor", False), kw.get("b_kmajor", False),
+                        kw.get("pro_a", 0) or kw.get("pro_b", 0), int(M), int(N), int(K), e0, e1))
+        kernels.gemm = timed
+        return self
+
+    def __exit__(self, *exc):
+        self.k.gemm = self.orig
+
+    def summary(self):
+        torch.cuda.synchronize()
+        by = {}
+        for epi, ak, bk, pro, M, N, K, e0, e1 in self.rec:
+            key = f"gemm<A_KM={int(ak)},B_KM={int(bk)},PRO={pro},EPI={epi}>"
+            ms = e0.elapsed_time(e1)
+            d = by.setdefault(key, {"launches": 0, "ms": 0.0, "flop": 0.0})
+            d["launches"] += 1
+            d["ms"] += ms
+            d["flop"] += 2.0 * M * N * K
+        return by
+
+
+def cpu_baseline(args, cfg_small_threads=16):
+    """The oracle (CPU restatement, torch fp32) timed on this host on a bounded sample."""
+    from oracle import ured_ref
+    from dataset import synthetic
+    threads = min(cfg_small_threads, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = workload_cfg(args)
+    P = ured_ref.make_params(cfg, seed=0)
+    for mod in P.values():
+        for k, v in mod.items():
+            if v.dtype.is_floating_point and "running" not in k:
+                v.requires_grad_(True)
+    ns = min(args.sources, 64)
+    db = synthetic.make_source_db(ns, seed=1)
+    bt = synthetic.make_batch(args.batch, args.points, ns, parts=args.parts, seed=0)
+    ob = {"src_points": torch.from_numpy(db["src_points"]), "src_mats": torch.from_numpy(db["src_mats"]),
+          "src_sem": torch.from_numpy(db["src_sem"]), "src_index": torch.from_numpy(bt["src_index"]),
+          "tgt_sem": torch.from_numpy(bt["tgt_sem"]), "x": torch.from_numpy(bt["x"]),
+          "labels": torch.from_numpy(bt["labels"]).float(),
+          "src_labels": torch.from_numpy(np.where(bt["src_labels"] >= 0, 1, bt["src_labels"]))}
+    params = [v for _, _, v in ured_ref.trainable(P)]
+    opt = torch.optim.Adam(params, lr=1e-3, weight_decay=5e-4)
+    t0 = time.time()
+    loss, _ = ured_ref.train_forward(P, ob, cfg)
+    loss.backward()
+    opt.step()
+    dt = time.time() - t0
+    return {"value": 1.0 / dt, "unit": "iters/s", "cores": threads, "kind": "port",
+            "sample": f"1 full oracle train step (fwd+bwd+Adam) at the bench shape bs={args.batch} "
+                      f"N={args.points} on {threads} host threads, {dt:.1f} s"}
+
+
+def chamfer_rate(dev, iters=20):
+    from ured_hip import nn as unn
+    g = torch.Generator().manual_seed(0)
+    p1 = torch.rand(16, 2048, 3, generator=g).to(dev)
+    p2 = torch.rand(16, 2048, 3, generator=g).to(dev)
+    for _ in range(3):
+        unn.nn_dense(p1, p2)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        unn.nn_dense(p1, p2)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / iters * 1e-3
+    return 16 * 2048 * 2048 / t / 1e9
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--points", type=int, default=2048)
+    ap.add_argument("--parts", type=int, default=4)
+    ap.add_argument("--sources", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-breakdown", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.manual_seed(1234 + rank)
+
+    ge.build()
+    from engine.dp import DataParallelStep
+    from engine.train import batch_to_device
+    from train_utils.load_sources import load_sources
+    from dataset import synthetic
+
+    cfg = workload_cfg(args)
+    db, _ = load_sources(cfg, dev)
+    step = DataParallelStep(cfg, db, dev)
+    batches = [batch_to_device(synthetic.make_batch(args.batch, args.points, db.num_sources, parts=args.parts,
+                                                    seed=1000 * rank + i), dev) for i in range(4)]
+
+    for i in range(args.warmup):
+        step.step(batches[i % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        T = step.step(batches[i % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    loss_val = float(T["all_loss"].item())
+
+    breakdown = None
+    if not args.no_breakdown:
+        with GemmTimer() as gt:
+            step.step(batches[0])
+        breakdown = gt.summary()
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    ms = elapsed / args.steps * 1e3
+    iters_per_s = args.steps / elapsed
+    roofline = None
+    extra = {}
+    if breakdown:
+        dom_key = max(breakdown, key=lambda k: breakdown[k]["ms"])
+        d = breakdown[dom_key]
+        avg_ms = d["ms"] / d["launches"]
+        flop_per_launch = d["flop"] / d["launches"]
+        ach = flop_per_launch / (avg_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None, "kernel": dom_key,
+                    "launches_per_step": d["launches"], "avg_launch_ms": round(avg_ms, 4)}
+        tot_ms = sum(v["ms"] for v in breakdown.values())
+        tot_flop = sum(v["flop"] for v in breakdown.values())
+        extra["gemm_all"] = {"ms_per_step": round(tot_ms, 3), "tflop_per_step": round(tot_flop / 1e12, 4),
+                             "tflops": round(tot_flop / (tot_ms * 1e-3) / 1e12, 2)}
+        extra["gemm_variants"] = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                                      "tflops": round(v["flop"] / max(v["ms"], 1e-9) / 1e9, 2)}
+                                  for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
+    extra["chamfer_gpair_s"] = round(chamfer_rate(dev), 1)
+    extra["loss"] = loss_val
+    cpu = None if args.no_cpu_baseline else cpu_baseline(args)
+    out = {"metric": "train iters/sec chair bs=16 2048-pt @1/2/4/8 GPU; Chamfer Gpair-dist/s",
+           "value": round(iters_per_s * world, 4), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY §8d generator; random-init weights)",
+           "config": {"workload": "config 2: chair, full U-RED train step, bs=16/GPU, 2048 pts, 16x1024 source pts, "
+                                  "C=512, S=128, 4 parts/target", "global_batch": args.batch * world,
+                      "points": args.points, "parallelism": f"dp{world}",
+                      "samples_per_s": round(iters_per_s * world * args.batch, 2)},
+           "roofline": roofline, "cpu_baseline": cpu}
+    out.update(extra)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
