@@ -50,126 +50,163 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 }
 
 // ---- operand staging -------------------------------------------------------
-// A "row-major" operand tile: ROWS (m or n) x BK (k) from G[row*ld + k]; k contiguous.
-// Staged into LDS transposed: S[k][row] with row stride LDP.
-// Thread t handles k4 = t % 8 (4 consecutive k) and rows t/8 + 32*i, i = 0..3.
-struct RowTile { float v[4][4]; };
+// Loads are branch-free: every lane loads from a clamped (always in-bounds) address and
+// out-of-range elements are zeroed by a select afterwards, so hipcc keeps all loads of a
+// tile in flight (a load under a per-lane branch gets its own vmcnt(0) wait).
+// VEC: float4 loads (requires 16-B aligned rows and contiguous extents multiple of 4).
+// A staged tile lives in registers between its loads (issued before the MFMAs of the
+// previous tile) and its LDS write (after them). The prologue transform and the
+// out-of-range zeroing are applied at write time so no wait sits in front of the MFMAs.
+struct RowTile {
+    float v[4][4];       // raw loaded values
+    float s[4], t[4];    // prologue affine of the 4 channels this thread stages (per c)
+    unsigned valid;      // bit 4*i+c
+    unsigned raw;        // bit 4*i+c: element comes from the raw second operand (no prologue)
+};
 
 template <int PRO>
+__device__ __forceinline__ float finish(const RowTile& r, int i, int c) {
+    float y = r.v[i][c];
+    if (PRO != URED_PRO_NONE) {
+        const float z = pro_apply(PRO, y, r.s[c], r.t[c]);
+        y = ((r.raw >> (4 * i + c)) & 1u) ? y : z;
+    }
+    return ((r.valid >> (4 * i + c)) & 1u) ? y : 0.f;
+}
+
+// "row-major" operand: rows (m or n) x BK (k) from G[row*ld + k]; k contiguous; staged
+// transposed to S[k][row]. Thread t: k4 = t % 8 (4 consecutive k), rows t/8 + 32*i.
+// k >= k1 reads the raw second operand A2[row*ld2 + k - k1] (concatenated input).
+template <int PRO, bool VEC>
 __device__ __forceinline__ void load_rowmajor(RowTile& r, const float* __restrict__ G, int ld, int rows, int row0,
                                               int K, int k0, const float* __restrict__ A2, int ld2, int k1,
-                                              const float* __restrict__ ps, const float* __restrict__ pt,
-                                              bool vec) {
+                                              const float* __restrict__ ps, const float* __restrict__ pt) {
     const int t = threadIdx.x, k4 = t & 7;
     const int kb = k0 + 4 * k4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = row0 + (t >> 3) + 32 * i;
-        float x[4] = {0.f, 0.f, 0.f, 0.f};
-        if (row < rows) {
-            if (vec && kb + 3 < K && (kb + 3 < k1 || kb >= k1)) {
-                if (kb < k1) {
-                    const float4 q = *reinterpret_cast<const float4*>(G + (size_t)row * ld + kb);
-                    x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
-                    if (PRO != URED_PRO_NONE) {
-                        const float4 s = *reinterpret_cast<const float4*>(ps + kb);
-                        const float4 tt = *reinterpret_cast<const float4*>(pt + kb);
-                        x[0] = pro_apply(PRO, x[0], s.x, tt.x); x[1] = pro_apply(PRO, x[1], s.y, tt.y);
-                        x[2] = pro_apply(PRO, x[2], s.z, tt.z); x[3] = pro_apply(PRO, x[3], s.w, tt.w);
-                    }
-                } else {
-                    const float4 q = *reinterpret_cast<const float4*>(A2 + (size_t)row * ld2 + (kb - k1));
-                    x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
-                }
-            } else {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int k = kb + c;
-                    if (k < K) {
-                        if (k < k1) {
-                            float v = G[(size_t)row * ld + k];
-                            if (PRO != URED_PRO_NONE) v = pro_apply(PRO, v, ps[k], pt[k]);
-                            x[c] = v;
-                        } else {
-                            x[c] = A2[(size_t)row * ld2 + (k - k1)];
-                        }
-                    }
-                }
-            }
+    r.valid = 0u;
+    r.raw = 0u;
+    if constexpr (VEC) {
+        const bool kv = kb < K;
+        const int kc = kv ? kb : K - 4;
+        const bool first = kc < k1;
+        if (PRO != URED_PRO_NONE) {
+            const int kp = first ? kc : k1 - 4;
+            const float4 s = *reinterpret_cast<const float4*>(ps + kp);
+            const float4 tt = *reinterpret_cast<const float4*>(pt + kp);
+            r.s[0] = s.x; r.s[1] = s.y; r.s[2] = s.z; r.s[3] = s.w;
+            r.t[0] = tt.x; r.t[1] = tt.y; r.t[2] = tt.z; r.t[3] = tt.w;
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) r.v[i][c] = x[c];
+        for (int i = 0; i < 4; ++i) {
+            const int row = row0 + (t >> 3) + 32 * i;
+            const int rc = row < rows ? row : rows - 1;
+            const float* src = first ? G + (size_t)rc * ld + kc : A2 + (size_t)rc * ld2 + (kc - k1);
+            const float4 q = *reinterpret_cast<const float4*>(src);
+            r.v[i][0] = q.x; r.v[i][1] = q.y; r.v[i][2] = q.z; r.v[i][3] = q.w;
+            const unsigned m = (kv && row < rows) ? 0xFu : 0u;
+            r.valid |= m << (4 * i);
+            r.raw |= (first ? 0u : 0xFu) << (4 * i);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int k = kb + c;
+            const int kc = k < K ? k : K - 1;
+            const bool first = kc < k1;
+            if (PRO != URED_PRO_NONE) {
+                const int kp = first ? kc : 0;
+                r.s[c] = ps[kp];
+                r.t[c] = pt[kp];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = row0 + (t >> 3) + 32 * i;
+                const int rc = row < rows ? row : rows - 1;
+                const float* src = first ? G + (size_t)rc * ld + kc : A2 + (size_t)rc * ld2 + (kc - k1);
+                r.v[i][c] = *src;
+                r.valid |= (k < K && row < rows ? 1u : 0u) << (4 * i + c);
+                r.raw |= (first ? 0u : 1u) << (4 * i + c);
+            }
+        }
     }
 }
 
-template <int LDP>
+template <int LDP, int PRO>
 __device__ __forceinline__ void store_rowmajor(const RowTile& r, float* S) {
     const int t = threadIdx.x, k4 = t & 7;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int row = (t >> 3) + 32 * i;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) S[(4 * k4 + c) * LDP + row] = r.v[i][c];
+        for (int c = 0; c < 4; ++c) S[(4 * k4 + c) * LDP + row] = finish<PRO>(r, i, c);
     }
 }
 
-// A "k-major" operand tile: BK (k) x COLS (m or n) from G[k*ld + col]; col contiguous.
-// Staged directly: S[k][col]. Thread t handles col4 = t % 32 and k = t/32 + 8*i.
-template <int PRO>
+// "k-major" operand: BK (k) x cols (m or n) from G[k*ld + col]; col contiguous; staged
+// directly to S[k][col]. Thread t: col4 = t % 32, k = t/32 + 8*i. The prologue channel is col.
+template <int PRO, bool VEC>
 __device__ __forceinline__ void load_kmajor(RowTile& r, const float* __restrict__ G, int ld, int cols, int col0,
                                             int K, int k0, const float* __restrict__ ps,
-                                            const float* __restrict__ pt, bool vec) {
+                                            const float* __restrict__ pt) {
     const int t = threadIdx.x, c4 = t & 31;
     const int cb = col0 + 4 * c4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int k = k0 + (t >> 5) + 8 * i;
-        float x[4] = {0.f, 0.f, 0.f, 0.f};
-        if (k < K) {
-            if (vec && cb + 3 < cols) {
-                const float4 q = *reinterpret_cast<const float4*>(G + (size_t)k * ld + cb);
-                x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
-                if (PRO != URED_PRO_NONE) {
-                    const float4 s = *reinterpret_cast<const float4*>(ps + cb);
-                    const float4 tt = *reinterpret_cast<const float4*>(pt + cb);
-                    x[0] = pro_apply(PRO, x[0], s.x, tt.x); x[1] = pro_apply(PRO, x[1], s.y, tt.y);
-                    x[2] = pro_apply(PRO, x[2], s.z, tt.z); x[3] = pro_apply(PRO, x[3], s.w, tt.w);
-                }
-            } else {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int col = cb + c;
-                    if (col < cols) {
-                        float v = G[(size_t)k * ld + col];
-                        if (PRO != URED_PRO_NONE) v = pro_apply(PRO, v, ps[col], pt[col]);
-                        x[c] = v;
-                    }
-                }
-            }
+    r.valid = 0u;
+    r.raw = 0u;
+    if constexpr (VEC) {
+        const bool cv = cb < cols;
+        const int cc = cv ? cb : cols - 4;
+        if (PRO != URED_PRO_NONE) {
+            const float4 s = *reinterpret_cast<const float4*>(ps + cc);
+            const float4 tt = *reinterpret_cast<const float4*>(pt + cc);
+            r.s[0] = s.x; r.s[1] = s.y; r.s[2] = s.z; r.s[3] = s.w;
+            r.t[0] = tt.x; r.t[1] = tt.y; r.t[2] = tt.z; r.t[3] = tt.w;
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) r.v[i][c] = x[c];
+        for (int i = 0; i < 4; ++i) {
+            const int k = k0 + (t >> 5) + 8 * i;
+            const int kc = k < K ? k : K - 1;
+            const float4 q = *reinterpret_cast<const float4*>(G + (size_t)kc * ld + cc);
+            r.v[i][0] = q.x; r.v[i][1] = q.y; r.v[i][2] = q.z; r.v[i][3] = q.w;
+            r.valid |= ((cv && k < K) ? 0xFu : 0u) << (4 * i);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int col = cb + c;
+            const int ccl = col < cols ? col : cols - 1;
+            if (PRO != URED_PRO_NONE) { r.s[c] = ps[ccl]; r.t[c] = pt[ccl]; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = k0 + (t >> 5) + 8 * i;
+                const int kc = k < K ? k : K - 1;
+                r.v[i][c] = G[(size_t)kc * ld + ccl];
+                r.valid |= (col < cols && k < K ? 1u : 0u) << (4 * i + c);
+            }
+        }
     }
 }
 
-template <int LDP>
+template <int LDP, int PRO>
 __device__ __forceinline__ void store_kmajor(const RowTile& r, float* S) {
     const int t = threadIdx.x, c4 = t & 31;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int k = (t >> 5) + 8 * i;
-        *reinterpret_cast<float4*>(S + k * LDP + 4 * c4) = make_float4(r.v[i][0], r.v[i][1], r.v[i][2], r.v[i][3]);
+        *reinterpret_cast<float4*>(S + k * LDP + 4 * c4) =
+            make_float4(finish<PRO>(r, i, 0), finish<PRO>(r, i, 1), finish<PRO>(r, i, 2), finish<PRO>(r, i, 3));
     }
 }
 
 template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; };
 
 // ---- the kernel ---------------------------------------------------------------
-template <bool A_KM, bool B_KM, int PRO_A, int PRO_B, int EPI>
+// Double-buffered LDS: tile t+1 is loaded to registers before the MFMAs of tile t and
+// written to the other buffer after them; one barrier per K-tile.
+template <bool A_KM, bool B_KM, int PRO_A, int PRO_B, int EPI, bool VEC>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
     constexpr int LDA = Pad<A_KM>::v, LDB = Pad<B_KM>::v;
-    __shared__ __attribute__((aligned(16))) float As[BK * LDA];
-    __shared__ __attribute__((aligned(16))) float Bs[BK * LDB];
+    constexpr int SA = BK * LDA, SB = BK * LDB;
+    __shared__ __attribute__((aligned(16))) float smem[2 * (SA + SB)];
     __shared__ float red[2][2][BN];       // [wm][quantity][col] cross-wave reductions
     __shared__ int redi[2][2][BN];
 
@@ -184,8 +221,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
         kend = min(d.K, kbeg + kps);
     }
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
-    const bool vecA = ((d.lda & 3) == 0) && (A_KM || ((d.k1 & 3) == 0 && (d.A2 == nullptr || (d.lda2 & 3) == 0)));
-    const bool vecB = (d.ldb & 3) == 0;
 
     f16v acc[2][2];
 #pragma unroll
@@ -197,23 +232,28 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
 
     RowTile ra, rb;
     auto load = [&](int k0) {
-        if (A_KM) load_kmajor<PRO_A>(ra, d.A, d.lda, d.M, m0, kend, k0, d.pro_s, d.pro_t, vecA);
-        else load_rowmajor<PRO_A>(ra, d.A, d.lda, d.M, m0, kend, k0, d.A2, d.lda2, d.k1, d.pro_s, d.pro_t, vecA);
-        if (B_KM) load_kmajor<PRO_B>(rb, d.B, d.ldb, d.N, n0, kend, k0, d.pro_s, d.pro_t, vecB);
-        else load_rowmajor<URED_PRO_NONE>(rb, d.B, d.ldb, d.N, n0, kend, k0, nullptr, 0, 0x7fffffff, nullptr, nullptr, vecB);
+        if constexpr (A_KM) load_kmajor<PRO_A, VEC>(ra, d.A, d.lda, d.M, m0, kend, k0, d.pro_s, d.pro_t);
+        else load_rowmajor<PRO_A, VEC>(ra, d.A, d.lda, d.M, m0, kend, k0, d.A2, d.lda2, d.k1, d.pro_s, d.pro_t);
+        if constexpr (B_KM) load_kmajor<PRO_B, VEC>(rb, d.B, d.ldb, d.N, n0, kend, k0, d.pro_s, d.pro_t);
+        else load_rowmajor<URED_PRO_NONE, VEC>(rb, d.B, d.ldb, d.N, n0, kend, k0, d.B, 0, 0x7fffffff, nullptr, nullptr);
     };
-    auto stage = [&]() {
-        if (A_KM) store_kmajor<LDA>(ra, As); else store_rowmajor<LDA>(ra, As);
-        if (B_KM) store_kmajor<LDB>(rb, Bs); else store_rowmajor<LDB>(rb, Bs);
+    auto stage = [&](int buf) {
+        float* As = smem + buf * (SA + SB);
+        float* Bs = As + SA;
+        if constexpr (A_KM) store_kmajor<LDA, PRO_A>(ra, As); else store_rowmajor<LDA, PRO_A>(ra, As);
+        if constexpr (B_KM) store_kmajor<LDB, PRO_B>(rb, Bs); else store_rowmajor<LDB, URED_PRO_NONE>(rb, Bs);
     };
 
     if (kbeg < kend) {
         load(kbeg);
+        stage(0);
+        __syncthreads();
+        int buf = 0;
         for (int k0 = kbeg; k0 < kend; k0 += BK) {
-            __syncthreads();
-            stage();
-            __syncthreads();
-            if (k0 + BK < kend) load(k0 + BK);   // prefetch: latency hidden under the MFMAs
+            const bool more = k0 + BK < kend;
+            if (more) load(k0 + BK);   // global loads in flight under this tile's MFMAs
+            const float* As = smem + buf * (SA + SB);
+            const float* Bs = As + SA;
             const float* ap = As + (lane >> 5) * LDA + wm * 64 + (lane & 31);
             const float* bp = Bs + (lane >> 5) * LDB + wn * 64 + (lane & 31);
 #pragma unroll
@@ -225,6 +265,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
                 acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
                 acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
             }
+            if (more) stage(buf ^ 1);   // the other buffer's last readers finished before the previous barrier
+            __syncthreads();
+            buf ^= 1;
         }
     }
 
@@ -618,11 +661,23 @@ __global__ __launch_bounds__(256) void group_colsum_kernel(const float* __restri
     if (w == 0 && n < N) out[(size_t)g * ldo + n] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
 }
 
+// VEC (float4 staging) needs 16-B aligned rows and contiguous extents that are multiples of 4.
+bool vec_ok(const UredGemmDesc& d) {
+    const bool a = (d.lda % 4 == 0) && (d.a_kmajor ? d.M % 4 == 0 : (d.K % 4 == 0 && d.k1 % 4 == 0 &&
+                   (d.k1 == d.K || d.lda2 % 4 == 0)));
+    const bool b = (d.ldb % 4 == 0) && (d.b_kmajor ? d.N % 4 == 0 : d.K % 4 == 0);
+    const bool p = !(d.pro_a || d.pro_b) || ((reinterpret_cast<uintptr_t>(d.pro_s) | reinterpret_cast<uintptr_t>(d.pro_t)) % 16 == 0);
+    const bool al = (reinterpret_cast<uintptr_t>(d.A) % 16 == 0) && (reinterpret_cast<uintptr_t>(d.B) % 16 == 0) &&
+                    (d.A2 == nullptr || reinterpret_cast<uintptr_t>(d.A2) % 16 == 0);
+    return a && b && p && al;
+}
+
 template <bool A_KM, bool B_KM, int PA, int PB, int EPI>
 void launch(const UredGemmDesc& d, hipStream_t st) {
     const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
     dim3 grid(ntm * ntn, 1, EPI == URED_EPI_SPLITK ? d.splits : 1);
-    hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI>), grid, dim3(NT), 0, st, d);
+    if (vec_ok(d)) hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, true>), grid, dim3(NT), 0, st, d);
+    else hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, false>), grid, dim3(NT), 0, st, d);
 }
 
 // The variants the MLP needs: forward (row-major A with prologue, row-major W),

@@ -1,9 +1,11 @@
 """The whole U-RED training step on the HIP path vs the CPU oracle (same weights, same batch).
 
-Tolerances: every loss term 2e-5 relative (north star: "loss within 1e-5 of
-reference"; the total is ~1e2, fp32 ulp there ~1e-5 relative); per-parameter
-gradient norms 2e-3 relative with a 1e-4 floor for the BN-cancelled biases
-(rounding noise on both sides); deformed shape 1e-4 relative.
+The oracle runs in float64 (weights and inputs; its chamfer primitive stays the
+fp32 contract formula). Tolerances: every loss term 2e-5 relative (north star:
+"loss within 1e-5 of reference"; the total is ~1e2, fp32 ulp there ~1e-5
+relative); per-parameter gradient norms 2e-3 relative; the BN-cancelled conv
+biases (true gradient exactly 0) only need to stay at noise level; deformed
+shape 1e-4 relative.
 """
 import numpy as np
 import pytest
@@ -38,10 +40,16 @@ def _setup(dev, B=2, N=128, parts=(3, 2), ns=24, seed=4):
           "tgt_sem": torch.from_numpy(bt["tgt_sem"]), "x": torch.from_numpy(bt["x"]),
           "labels": torch.from_numpy(bt["labels"]).float(), "src_labels": torch.from_numpy(bt["src_labels"])}
     ob["src_labels"] = torch.where(ob["src_labels"] >= 0, torch.ones_like(ob["src_labels"]), ob["src_labels"])
+    # the oracle runs in float64: early-layer gradient norms of an fp32 CPU run carry ~2e-3 of
+    # rounding noise at these sizes (measured), more than the HIP path (fp64 BN statistics)
     for mod in P.values():
-        for k, v in mod.items():
-            if v.dtype.is_floating_point and "running" not in k:
-                v.requires_grad_(True)
+        for k in list(mod):
+            if mod[k].dtype.is_floating_point:
+                mod[k] = mod[k].double()
+                if "running" not in k:
+                    mod[k].requires_grad_(True)
+    for k in ("src_points", "src_mats", "x", "labels"):
+        ob[k] = ob[k].double()
     return ts, batch, P, ob, cfg
 
 
