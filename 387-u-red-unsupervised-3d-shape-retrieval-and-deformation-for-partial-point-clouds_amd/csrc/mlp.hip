@@ -24,6 +24,7 @@
 //    parallel variance, order-fixed, deterministic), max-pool partials, the
 //    BN-backward masks/partials of the previous layer, or split-K partials;
 //  * XCD-aware tile order: blocks that share an A row-panel run on one XCD.
+#include <cstdlib>
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -199,79 +200,14 @@ __device__ __forceinline__ void store_kmajor(const RowTile& r, float* S) {
 
 template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; };
 
-// ---- the kernel ---------------------------------------------------------------
-// Double-buffered LDS: tile t+1 is loaded to registers before the MFMAs of tile t and
-// written to the other buffer after them; one barrier per K-tile.
-template <bool A_KM, bool B_KM, int PRO_A, int PRO_B, int EPI, bool VEC>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
-    constexpr int LDA = Pad<A_KM>::v, LDB = Pad<B_KM>::v;
-    constexpr int SA = BK * LDA, SB = BK * LDB;
-    __shared__ __attribute__((aligned(16))) float smem[2 * (SA + SB)];
-    __shared__ float red[2][2][BN];       // [wm][quantity][col] cross-wave reductions
-    __shared__ int redi[2][2][BN];
-
-    const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
-    const int tile = xcd_remap(blockIdx.x, ntm * ntn);
-    const int tm_ = tile / ntn, tn_ = tile % ntn;
-    const int m0 = tm_ * BM, n0 = tn_ * BN;
-    int kbeg = 0, kend = d.K;
-    if (EPI == URED_EPI_SPLITK) {
-        const int kps = ((d.K + d.splits - 1) / d.splits + BK - 1) / BK * BK;
-        kbeg = blockIdx.z * kps;
-        kend = min(d.K, kbeg + kps);
-    }
+// ---- shared epilogue ---------------------------------------------------------
+// element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
+#define RED(a, q, c) red_f[((a) * 2 + (q)) * BN + (c)]
+#define REDI(a, q, c) red_i[((a) * 2 + (q)) * BN + (c)]
+template <int EPI>
+__device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2], int m0, int n0,
+                                         float* red_f, int* red_i) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
-
-    f16v acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    RowTile ra, rb;
-    auto load = [&](int k0) {
-        if constexpr (A_KM) load_kmajor<PRO_A, VEC>(ra, d.A, d.lda, d.M, m0, kend, k0, d.pro_s, d.pro_t);
-        else load_rowmajor<PRO_A, VEC>(ra, d.A, d.lda, d.M, m0, kend, k0, d.A2, d.lda2, d.k1, d.pro_s, d.pro_t);
-        if constexpr (B_KM) load_kmajor<PRO_B, VEC>(rb, d.B, d.ldb, d.N, n0, kend, k0, d.pro_s, d.pro_t);
-        else load_rowmajor<URED_PRO_NONE, VEC>(rb, d.B, d.ldb, d.N, n0, kend, k0, d.B, 0, 0x7fffffff, nullptr, nullptr);
-    };
-    auto stage = [&](int buf) {
-        float* As = smem + buf * (SA + SB);
-        float* Bs = As + SA;
-        if constexpr (A_KM) store_kmajor<LDA, PRO_A>(ra, As); else store_rowmajor<LDA, PRO_A>(ra, As);
-        if constexpr (B_KM) store_kmajor<LDB, PRO_B>(rb, Bs); else store_rowmajor<LDB, URED_PRO_NONE>(rb, Bs);
-    };
-
-    if (kbeg < kend) {
-        load(kbeg);
-        stage(0);
-        __syncthreads();
-        int buf = 0;
-        for (int k0 = kbeg; k0 < kend; k0 += BK) {
-            const bool more = k0 + BK < kend;
-            if (more) load(k0 + BK);   // global loads in flight under this tile's MFMAs
-            const float* As = smem + buf * (SA + SB);
-            const float* Bs = As + SA;
-            const float* ap = As + (lane >> 5) * LDA + wm * 64 + (lane & 31);
-            const float* bp = Bs + (lane >> 5) * LDB + wn * 64 + (lane & 31);
-#pragma unroll
-            for (int kk = 0; kk < BK / 2; ++kk) {
-                const float a0 = ap[2 * kk * LDA], a1 = ap[2 * kk * LDA + 32];
-                const float b0 = bp[2 * kk * LDB], b1 = bp[2 * kk * LDB + 32];
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-            }
-            if (more) stage(buf ^ 1);   // the other buffer's last readers finished before the previous barrier
-            __syncthreads();
-            buf ^= 1;
-        }
-    }
-
-    // ---- epilogues --------------------------------------------------------------
     // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
     const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
     auto row_of = [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); };
@@ -337,14 +273,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
         }
         if (lane < 32) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) red[wm][0][wn * 64 + j * 32 + lane] = csum[j];
+            for (int j = 0; j < 2; ++j) RED(wm, 0, wn * 64 + j * 32 + lane) = csum[j];
         }
         __syncthreads();
         float cmean[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int c = wn * 64 + j * 32 + (lane & 31);
-            cmean[j] = (red[0][0][c] + red[1][0][c]) / (float)nvalid;
+            cmean[j] = (RED(0, 0, c) + RED(1, 0, c)) / (float)nvalid;
         }
         // pass 2: M2 about the block mean
         float cm2[2];
@@ -364,7 +300,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
         }
         if (lane < 32) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) red[wm][1][wn * 64 + j * 32 + lane] = cm2[j];
+            for (int j = 0; j < 2; ++j) RED(wm, 1, wn * 64 + j * 32 + lane) = cm2[j];
         }
         __syncthreads();
         if (wm == 0 && lane < 32) {
@@ -374,7 +310,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
                 const int col = n0 + c;
                 if (col < d.N) {
                     d.stat_ws[(size_t)blk * 2 * d.N + col] = cmean[j];
-                    d.stat_ws[(size_t)blk * 2 * d.N + d.N + col] = red[0][1][c] + red[1][1][c];
+                    d.stat_ws[(size_t)blk * 2 * d.N + d.N + col] = RED(0, 1, c) + RED(1, 1, c);
                 }
             }
         }
@@ -405,8 +341,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     const int c = wn * 64 + j * 32 + lane;
-                    red[wm][0][c] = mx[j]; redi[wm][0][c] = ix[j];
-                    red[wm][1][c] = mn[j]; redi[wm][1][c] = in_[j];
+                    RED(wm, 0, c) = mx[j]; REDI(wm, 0, c) = ix[j];
+                    RED(wm, 1, c) = mn[j]; REDI(wm, 1, c) = in_[j];
                 }
             }
             __syncthreads();
@@ -416,10 +352,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
                     const int c = wn * 64 + j * 32 + lane;
                     const int col = n0 + c;
                     if (col >= d.N) continue;
-                    float a = red[0][0][c]; int ai = redi[0][0][c];
-                    if (red[1][0][c] > a || (red[1][0][c] == a && redi[1][0][c] < ai)) { a = red[1][0][c]; ai = redi[1][0][c]; }
-                    float b = red[0][1][c]; int bi = redi[0][1][c];
-                    if (red[1][1][c] < b || (red[1][1][c] == b && redi[1][1][c] < bi)) { b = red[1][1][c]; bi = redi[1][1][c]; }
+                    float a = RED(0, 0, c); int ai = REDI(0, 0, c);
+                    if (RED(1, 0, c) > a || (RED(1, 0, c) == a && REDI(1, 0, c) < ai)) { a = RED(1, 0, c); ai = REDI(1, 0, c); }
+                    float b = RED(0, 1, c); int bi = REDI(0, 1, c);
+                    if (RED(1, 1, c) < b || (RED(1, 1, c) == b && REDI(1, 1, c) < bi)) { b = RED(1, 1, c); bi = REDI(1, 1, c); }
                     float* pw = d.pool_ws + (size_t)blk * 4 * d.N;
                     pw[col] = a; reinterpret_cast<int*>(pw)[d.N + col] = ai;
                     pw[2 * d.N + col] = b; reinterpret_cast<int*>(pw)[3 * d.N + col] = bi;
@@ -476,8 +412,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
         if (lane < 32) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                red[wm][0][wn * 64 + j * 32 + lane] = s1[j];
-                red[wm][1][wn * 64 + j * 32 + lane] = s2[j];
+                RED(wm, 0, wn * 64 + j * 32 + lane) = s1[j];
+                RED(wm, 1, wn * 64 + j * 32 + lane) = s2[j];
             }
         }
         __syncthreads();
@@ -487,12 +423,277 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
                 const int c = wn * 64 + j * 32 + lane;
                 const int col = n0 + c;
                 if (col < d.N) {
-                    d.bwd_ws[(size_t)blk * 2 * d.N + col] = red[0][0][c] + red[1][0][c];
-                    d.bwd_ws[(size_t)blk * 2 * d.N + d.N + col] = red[0][1][c] + red[1][1][c];
+                    d.bwd_ws[(size_t)blk * 2 * d.N + col] = RED(0, 0, c) + RED(1, 0, c);
+                    d.bwd_ws[(size_t)blk * 2 * d.N + d.N + col] = RED(0, 1, c) + RED(1, 1, c);
                 }
             }
         }
     }
+}
+#undef RED
+#undef REDI
+
+// ---- the kernel ---------------------------------------------------------------
+// Double-buffered LDS: tile t+1 is loaded to registers before the MFMAs of tile t and
+// written to the other buffer after them; one barrier per K-tile.
+template <bool A_KM, bool B_KM, int PRO_A, int PRO_B, int EPI, bool VEC>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
+    constexpr int LDA = Pad<A_KM>::v, LDB = Pad<B_KM>::v;
+    constexpr int SA = BK * LDA, SB = BK * LDB;
+    __shared__ __attribute__((aligned(16))) float smem[2 * (SA + SB)];
+    __shared__ float red_f[4 * BN];       // [wm][quantity][col] cross-wave reductions
+    __shared__ int red_i[4 * BN];
+
+    const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
+    const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+    const int tm_ = tile / ntn, tn_ = tile % ntn;
+    const int m0 = tm_ * BM, n0 = tn_ * BN;
+    int kbeg = 0, kend = d.K;
+    if (EPI == URED_EPI_SPLITK) {
+        const int kps = ((d.K + d.splits - 1) / d.splits + BK - 1) / BK * BK;
+        kbeg = blockIdx.z * kps;
+        kend = min(d.K, kbeg + kps);
+    }
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
+
+    f16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    RowTile ra, rb;
+    auto load = [&](int k0) {
+        if constexpr (A_KM) load_kmajor<PRO_A, VEC>(ra, d.A, d.lda, d.M, m0, kend, k0, d.pro_s, d.pro_t);
+        else load_rowmajor<PRO_A, VEC>(ra, d.A, d.lda, d.M, m0, kend, k0, d.A2, d.lda2, d.k1, d.pro_s, d.pro_t);
+        if constexpr (B_KM) load_kmajor<PRO_B, VEC>(rb, d.B, d.ldb, d.N, n0, kend, k0, d.pro_s, d.pro_t);
+        else load_rowmajor<URED_PRO_NONE, VEC>(rb, d.B, d.ldb, d.N, n0, kend, k0, d.B, 0, 0x7fffffff, nullptr, nullptr);
+    };
+    auto stage = [&](int buf) {
+        float* As = smem + buf * (SA + SB);
+        float* Bs = As + SA;
+        if constexpr (A_KM) store_kmajor<LDA, PRO_A>(ra, As); else store_rowmajor<LDA, PRO_A>(ra, As);
+        if constexpr (B_KM) store_kmajor<LDB, PRO_B>(rb, Bs); else store_rowmajor<LDB, URED_PRO_NONE>(rb, Bs);
+    };
+
+    if (kbeg < kend) {
+        load(kbeg);
+        stage(0);
+        __syncthreads();
+        int buf = 0;
+        for (int k0 = kbeg; k0 < kend; k0 += BK) {
+            const bool more = k0 + BK < kend;
+            if (more) load(k0 + BK);   // global loads in flight under this tile's MFMAs
+            const float* As = smem + buf * (SA + SB);
+            const float* Bs = As + SA;
+            const float* ap = As + (lane >> 5) * LDA + wm * 64 + (lane & 31);
+            const float* bp = Bs + (lane >> 5) * LDB + wn * 64 + (lane & 31);
+#pragma unroll
+            for (int kk = 0; kk < BK / 2; ++kk) {
+                const float a0 = ap[2 * kk * LDA], a1 = ap[2 * kk * LDA + 32];
+                const float b0 = bp[2 * kk * LDB], b1 = bp[2 * kk * LDB + 32];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            }
+            if (more) stage(buf ^ 1);   // the other buffer's last readers finished before the previous barrier
+            __syncthreads();
+            buf ^= 1;
+        }
+    }
+
+    epilogue<EPI>(d, acc, m0, n0, red_f, red_i);
+}
+
+
+// ---- v2: LDS-DMA staged kernel (all-VEC shapes) --------------------------------
+// Both operands reach LDS by global_load_lds_dwordx4 (no VGPR round trip, no staging
+// registers): a row-major [rows][k] operand lands as a [128][32] image with its 16-B
+// slots XOR-swizzled by (row & 7) (swizzle applied to the per-lane SOURCE address, the
+// LDS image stays lane-linear) and is read 4 consecutive k per ds_read_b128; a k-major
+// [k][cols] operand lands as a plain [32][128] image and is read with ds_read_b32.
+// The MFMA k-order is permuted (k-step j of lane half h uses k = 16h + j) so both image
+// kinds feed the same 32x32x2 sequence. The previous layer's BatchNorm+ReLU prologue is
+// applied to the fragments after the LDS read (one fma+max per operand element, hidden
+// under the 64-cycle MFMAs). Two LDS stages, the next tile's DMA in flight during the
+// current tile's MFMAs, one barrier per K-tile.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __forceinline__ void dma16(const float* src, float* lds_base) {
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_base, 16, 0, 0);
+}
+
+// 1024 16-B chunks per 128x32 tile; wave w issues chunks [w*256, w*256+256) as 4 DMAs.
+template <bool KM>
+__device__ __forceinline__ void dma_tile(const float* __restrict__ G, int ld, int ext, int e0, int K, int k0,
+                                         const float* __restrict__ A2, int ld2, int k1, float* S, int w, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int wi = w * 4 + i;
+        const int c = wi * 64 + lane;
+        const float* src;
+        if constexpr (!KM) {
+            const int r = c >> 3, p = c & 7, sl = p ^ (r & 7);
+            int row = e0 + r;
+            row = row < ext ? row : ext - 1;
+            int k = k0 + 4 * sl;
+            k = k < K ? k : K - 4;
+            src = k < k1 ? G + (size_t)row * ld + k : A2 + (size_t)row * ld2 + (k - k1);
+        } else {
+            const int kk = c >> 5, c4 = c & 31;
+            int k = k0 + kk;
+            k = k < K ? k : K - 1;
+            int col = e0 + 4 * c4;
+            col = col < ext ? col : ext - 4;
+            src = G + (size_t)k * ld + col;
+        }
+        dma16(src, S + wi * 256);
+    }
+}
+
+template <int PRO>
+__device__ __forceinline__ float pro_v(float x, float s, float t) {
+    if (PRO == URED_PRO_ENC) return fmaxf(__builtin_fmaf(x, s, t), 0.f);
+    if (PRO == URED_PRO_RES) return __builtin_fmaf(fmaxf(x, 0.f), s, t);
+    return x;
+}
+
+template <bool A_KM, bool B_KM, int PRO_A, int PRO_B, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
+    constexpr int TILE = BM * BK;                  // floats per operand image
+    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * TILE + 4 * BN];
+    float* red_f = smem + 4 * TILE;                // epilogue scratch (after the stages are drained)
+    int* red_i = reinterpret_cast<int*>(smem);     // pool scratch reuses stage 0 (drained by then)
+
+    const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
+    const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+    const int tm_ = tile / ntn, tn_ = tile % ntn;
+    const int m0 = tm_ * BM, n0 = tn_ * BN;
+    int kbeg = 0, kend = d.K;
+    if (EPI == URED_EPI_SPLITK) {
+        const int kps = ((d.K + d.splits - 1) / d.splits + BK - 1) / BK * BK;
+        kbeg = blockIdx.z * kps;
+        kend = min(d.K, kbeg + kps);
+    }
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
+    const int h = lane >> 5, li = lane & 31;
+
+    f16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // k-major B with prologue (wgrad): the channel is this lane's output column, fixed
+    float bs_[2] = {1.f, 1.f}, bt_[2] = {0.f, 0.f};
+    if (PRO_B != URED_PRO_NONE) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            int c = n0 + wn * 64 + j * 32 + li;
+            c = c < d.N ? c : d.N - 1;
+            bs_[j] = d.pro_s[c]; bt_[j] = d.pro_t[c];
+        }
+    }
+
+    auto issue = [&](int stage, int k0) {
+        float* As = smem + stage * 2 * TILE;
+        float* Bs = As + TILE;
+        dma_tile<A_KM>(d.A, d.lda, d.M, m0, kend, k0, d.A2, d.lda2, d.k1, As, w, lane);
+        dma_tile<B_KM>(d.B, d.ldb, d.N, n0, kend, k0, d.B, 0, 0x7fffffff, Bs, w, lane);
+    };
+
+    if (kbeg < kend) {
+        issue(0, kbeg);
+        int stage = 0;
+        for (int k0 = kbeg; k0 < kend; k0 += BK) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (k0 + BK < kend) issue(stage ^ 1, k0 + BK);   // lands while this tile is multiplied
+            const float* As = smem + stage * 2 * TILE;
+            const float* Bs = As + TILE;
+            const bool tail = k0 + BK > kend;
+
+            // ---- A fragments: a[tm][j] for k = k0 + 16h + j
+            float a[2][16];
+            if constexpr (!A_KM) {
+                float as_[16], at_[16];
+                bool raw = false;
+                if (PRO_A != URED_PRO_NONE) {
+                    int kc = k0 + 16 * h;
+                    raw = kc >= d.k1;
+                    kc = raw ? d.k1 - 16 : kc;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 sv = *reinterpret_cast<const float4*>(d.pro_s + kc + 4 * q);
+                        const float4 tv = *reinterpret_cast<const float4*>(d.pro_t + kc + 4 * q);
+                        as_[4 * q] = sv.x; as_[4 * q + 1] = sv.y; as_[4 * q + 2] = sv.z; as_[4 * q + 3] = sv.w;
+                        at_[4 * q] = tv.x; at_[4 * q + 1] = tv.y; at_[4 * q + 2] = tv.z; at_[4 * q + 3] = tv.w;
+                    }
+                }
+#pragma unroll
+                for (int tm = 0; tm < 2; ++tm) {
+                    const int r = wm * 64 + tm * 32 + li;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 v = *reinterpret_cast<const float4*>(As + r * 32 + 4 * ((4 * h + q) ^ (r & 7)));
+                        a[tm][4 * q] = v.x; a[tm][4 * q + 1] = v.y; a[tm][4 * q + 2] = v.z; a[tm][4 * q + 3] = v.w;
+                    }
+                    if (PRO_A != URED_PRO_NONE) {
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) a[tm][j] = raw ? a[tm][j] : pro_v<PRO_A>(a[tm][j], as_[j], at_[j]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) a[tm][j] = As[(16 * h + j) * BM + wm * 64 + tm * 32 + li];
+            }
+            if (tail) {   // zero the k >= K part of the reduction (the images hold clamped copies)
+#pragma unroll
+                for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) a[tm][j] = (k0 + 16 * h + j < kend) ? a[tm][j] : 0.f;
+            }
+            // ---- B fragments + MFMAs
+#pragma unroll
+            for (int jq = 0; jq < 4; ++jq) {
+                float b[2][4];
+#pragma unroll
+                for (int tn = 0; tn < 2; ++tn) {
+                    const int cidx = wn * 64 + tn * 32 + li;
+                    if constexpr (!B_KM) {
+                        const float4 v = *reinterpret_cast<const float4*>(Bs + cidx * 32 + 4 * ((4 * h + jq) ^ (cidx & 7)));
+                        b[tn][0] = v.x; b[tn][1] = v.y; b[tn][2] = v.z; b[tn][3] = v.w;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float x = Bs[(16 * h + 4 * jq + e) * BN + cidx];
+                            if (PRO_B != URED_PRO_NONE) x = pro_v<PRO_B>(x, bs_[tn], bt_[tn]);
+                            b[tn][e] = x;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int j = 4 * jq + e;
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[0][e], acc[0][0], 0, 0, 0);
+                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[1][e], acc[0][1], 0, 0, 0);
+                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[0][e], acc[1][0], 0, 0, 0);
+                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][e], acc[1][1], 0, 0, 0);
+                }
+            }
+            stage ^= 1;
+        }
+        __syncthreads();   // all waves done with the stages before the epilogue reuses LDS
+    }
+    epilogue<EPI>(d, acc, m0, n0, red_f, red_i);
 }
 
 // ---- small kernels -------------------------------------------------------------
@@ -672,11 +873,25 @@ bool vec_ok(const UredGemmDesc& d) {
     return a && b && p && al;
 }
 
+// v2 additionally needs the A prologue channels to come in 16-aligned runs (k1 % 16 == 0) and
+// rows/extents >= 4 so clamped 16-B sources stay in bounds.
+bool v2_enabled() {
+    static const bool on = [] { const char* e = getenv("URED_GEMM_V1"); return !(e && e[0] == '1'); }();
+    return on;
+}
+bool v2_ok(const UredGemmDesc& d) {
+    if (!v2_enabled()) return false;
+    if (d.pro_a && (d.k1 % 16 != 0)) return false;
+    if (d.K < 4 || (d.a_kmajor && d.M < 4) || (d.b_kmajor && d.N < 4)) return false;
+    return true;
+}
+
 template <bool A_KM, bool B_KM, int PA, int PB, int EPI>
 void launch(const UredGemmDesc& d, hipStream_t st) {
     const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
     dim3 grid(ntm * ntn, 1, EPI == URED_EPI_SPLITK ? d.splits : 1);
-    if (vec_ok(d)) hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, true>), grid, dim3(NT), 0, st, d);
+    if (vec_ok(d) && v2_ok(d)) hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI>), grid, dim3(NT), 0, st, d);
+    else if (vec_ok(d)) hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, true>), grid, dim3(NT), 0, st, d);
     else hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, false>), grid, dim3(NT), 0, st, d);
 }
 

@@ -1,0 +1,85 @@
+"""Retrieval + deformation inference (the working form of the reference's inference path).
+
+The reference's engine/test.py no longer runs against its own modules; the
+working path is engine/vis.py:118-256, restated here batched and without host syncs:
+  1. encode the whole source-part DB with src_encoder_all in eval mode (chunks of 512 parts,
+     vis.py:126-145) -> L2-normalised codes [NS, C]
+  2. encode the targets (eval), pool per-part features (vis.py:175-195), L2-normalise
+  3. cosine similarity target parts x sources, argmax -> retrieved source per part (vis.py:197-205)
+  4. DeformNet on (target code, normalised retrieved codes) -> params; get_shape with the
+     retrieved sources' A matrices and no default param (vis.py:243-252)
+  5. chamfer of the deformed shape (all 16x1024 points, the unmasked branch vis.py:256 lands in)
+    python engine/test.py [config.json]
+"""
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if os.path.dirname(_HERE) not in sys.path:
+    sys.path.insert(0, os.path.dirname(_HERE))
+
+from dataset import synthetic  # noqa: E402
+from dataset.dataset_utils import get_shape  # noqa: E402
+from engine.train import batch_to_device, get_models, get_part  # noqa: E402
+from loss.chamfer_loss import compute_cm_loss  # noqa: E402
+from train_utils.load_sources import load_sources  # noqa: E402
+
+
+@torch.no_grad()
+def encode_sources(models, db, chunk=512):
+    enc = models["src_encoder_all"]
+    emb = models["embedding_layer"]
+    codes = []
+    for s in range(0, db.num_sources, chunk):
+        pts = db.points[s:s + chunk].unsqueeze(1)                  # [n, 1, 1024, 3]
+        sem = emb(db.sem[s:s + chunk]).unsqueeze(1)                # [n, 1, S]
+        c, _ = enc.forward_pointmajor(pts, sem)
+        codes.append(c)
+    return F.normalize(torch.cat(codes), dim=-1, p=2)
+
+
+@torch.no_grad()
+def infer(models, db, batch, cfg, src_codes=None):
+    """-> dict(retrieved [B,P] (-1 for empty slots), sim_top2_gap [B,P], params [B,P,6],
+    out [B,P*1024,3], cd [B] (chamfer_distance2 of out vs x))."""
+    for m in models.values():
+        m.eval()
+    if src_codes is None:
+        src_codes = encode_sources(models, db)
+    x = batch["x"]
+    B, N, _ = x.shape
+    P = cfg["MAX_NUM_PARTS"]
+    tcode, pp = models["target_encoder_full"].forward_pointmajor(x, models["embedding_layer"](batch["tgt_sem"]))
+    part_f, _, _, mask, _, _ = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
+    part_n = F.normalize(part_f, dim=-1, p=2)
+    sim = part_n @ src_codes.t()                                      # [B, P, NS]
+    top2 = sim.topk(2, dim=-1).values
+    retrieved = sim.argmax(dim=-1)
+    retrieved = torch.where(mask > 0, retrieved, torch.full_like(retrieved, -1))
+    idx = torch.where(retrieved < 0, retrieved + db.num_sources, retrieved)
+    params = models["param_decoder_full"](tcode, src_codes[idx], None)
+    out = get_shape(db.mats[idx], params, None, cfg["alpha"]).reshape(B, -1, 3)
+    cd = compute_cm_loss(out, x, mask, batch_reduction=None)          # unmasked branch, like vis.py:256
+    return {"retrieved": retrieved, "sim_top2_gap": top2[..., 0] - top2[..., 1], "params": params,
+            "out": out, "cd": cd, "mask": mask}
+
+
+def main(cfg):
+    device = cfg["device"]
+    db, _ = load_sources(cfg, device)
+    models, _, _ = get_models(cfg, device)
+    codes = encode_sources(models, db)
+    for i in range(int(cfg.get("iters_per_epoch", 2))):
+        b = synthetic.make_batch(cfg["batch_size"], cfg.get("num_points", 2048), db.num_sources,
+                                 max_parts=cfg["MAX_NUM_PARTS"], parts=cfg.get("parts", 4), seed=10_000 + i)
+        r = infer(models, db, batch_to_device(b, device), cfg, codes)
+        print(i, "cd", r["cd"].mean().item(), "retrieved[0]", r["retrieved"][0].tolist())
+
+
+if __name__ == "__main__":
+    path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(_HERE), "config", "config_train_test.json")
+    main(json.load(open(path)))

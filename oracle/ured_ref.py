@@ -434,3 +434,35 @@ def trainable(params):
             if v.dtype.is_floating_point and not (k.endswith("running_mean") or k.endswith("running_var")):
                 out.append((mod, k, v))
     return out
+
+
+# ----------------------------------------------------------------------------
+# inference (engine/vis.py:118-256, batched)
+# ----------------------------------------------------------------------------
+
+def infer(params, batch, cfg, chunk=512):
+    """Retrieval + deformation in eval mode. batch holds src_points/src_mats/src_sem (the whole DB),
+    x, labels, tgt_sem. Returns retrieved [B,P] (-1 for empty slots), top-2 gap, params, out, cd [B]."""
+    with torch.no_grad():
+        emb = params["embedding_layer"]["weight"]
+        pts, sem = batch["src_points"], batch["src_sem"]
+        codes = []
+        for s in range(0, pts.shape[0], chunk):
+            c, _ = target_encoder(params["src_encoder_all"], pts[s:s + chunk].unsqueeze(1),
+                                  emb[sem[s:s + chunk]].unsqueeze(1), True, training=False)
+            codes.append(c)
+        codes = F.normalize(torch.cat(codes), dim=-1, p=2)
+        x = batch["x"]
+        B = x.shape[0]
+        P = cfg["MAX_NUM_PARTS"]
+        tcode, pp = target_encoder(params["target_encoder_full"], x, emb[batch["tgt_sem"]], False, training=False)
+        part_f, _, mask, _, _ = get_part(pp.permute(0, 2, 1), batch["labels"], x, P)
+        sim = F.normalize(part_f, dim=-1, p=2) @ codes.t()
+        top2 = sim.topk(2, dim=-1).values
+        retrieved = torch.where(mask > 0, sim.argmax(-1), torch.full((B, P), -1, dtype=torch.long))
+        idx = torch.where(retrieved < 0, retrieved + pts.shape[0], retrieved)
+        prm = deform_net(params["param_decoder_full"], tcode, codes[idx], training=False)
+        out = get_shape(batch["src_mats"][idx], prm, torch.zeros_like(prm), cfg["alpha"]).reshape(B, -1, 3)
+        cd = chamfer_distance2(out, x)
+        return {"retrieved": retrieved, "sim_top2_gap": top2[..., 0] - top2[..., 1], "params": prm,
+                "out": out, "cd": cd}
