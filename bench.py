@@ -55,7 +55,7 @@ class GemmTimer:
             self.orig(M, N, K, *a, **kw)
             e1.record()
             rec.append((kw.get("epi", 0), kw.get("a_kmajor", False), kw.get("b_kmajor", False),
-                        kw.get("pro_a", 0) or kw.get("pro_b", 0), int(M), int(N), int(K), e0, e1))
+                        kw.get("pro_a", 0), kw.get("pro_b", 0), int(M), int(N), int(K), e0, e1))
         kernels.gemm = timed
         return self
 
@@ -65,13 +65,18 @@ class GemmTimer:
     def summary(self):
         torch.cuda.synchronize()
         by = {}
-        for epi, ak, bk, pro, M, N, K, e0, e1 in self.rec:
-            key = f"gemm<A_KM={int(ak)},B_KM={int(bk)},PRO={pro},EPI={epi}>"
+        tf = {False: "false", True: "true"}
+        for epi, ak, bk, pa, pb, M, N, K, e0, e1 in self.rec:
+            key = f"gemm2_kernel<{tf[bool(ak)]}, {tf[bool(bk)]}, {pa}, {pb}, {epi}>"
             ms = e0.elapsed_time(e1)
-            d = by.setdefault(key, {"launches": 0, "ms": 0.0, "flop": 0.0})
+            d = by.setdefault(key, {"launches": 0, "ms": 0.0, "flop": 0.0, "bytes": 0.0})
             d["launches"] += 1
             d["ms"] += ms
             d["flop"] += 2.0 * M * N * K
+            # algorithmic HBM bytes: both operands once, the output once, the epilogue's extra
+            # read of the previous layer's output (BN backward) or the split partials
+            extra = 4.0 * M * N if epi == 2 else 0.0
+            d["bytes"] += 4.0 * (M * K + K * N + M * N) + extra
         return by
 
 
@@ -200,9 +205,19 @@ def main():
         avg_ms = d["ms"] / d["launches"]
         flop_per_launch = d["flop"] / d["launches"]
         ach = flop_per_launch / (avg_ms * 1e-3) / 1e12
+        traffic, tsrc = None, None
+        pmc = os.path.join(ROOT, "profiles", "r1_pmc_summary.json")
+        if os.path.exists(pmc):
+            pm = json.load(open(pmc))
+            for kname, v in pm.items():
+                if dom_key in kname:
+                    traffic, tsrc = v["hbm_bytes_per_launch"], os.path.relpath(pmc, ROOT)
         roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None, "kernel": dom_key,
-                    "launches_per_step": d["launches"], "avg_launch_ms": round(avg_ms, 4)}
+                    "frac": round(ach / PEAK_FP32_TFLOPS, 4),
+                    "traffic": None if traffic is None else round(traffic), "traffic_source": tsrc,
+                    "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
+                    "kernel": dom_key, "launches_per_step": d["launches"], "avg_launch_ms": round(avg_ms, 4),
+                    "flop_per_launch": round(flop_per_launch)}
         tot_ms = sum(v["ms"] for v in breakdown.values())
         tot_flop = sum(v["flop"] for v in breakdown.values())
         extra["gemm_all"] = {"ms_per_step": round(tot_ms, 3), "tflop_per_step": round(tot_flop / 1e12, 4),
