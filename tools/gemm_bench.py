@@ -1,0 +1,79 @@
+"""Micro-benchmark of ured_gemm on the U-RED step's dominant layer shapes (config 2).
+
+  python tools/gemm_bench.py [--iters 20]
+Prints TFLOP/s per (shape, variant); interleaves variants in one process (rule 24).
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+ge.add_pkg_path()
+from ured_hip import kernels as K  # noqa: E402
+
+SHAPES = [  # (name, M, N, K)  — source encoder (M = 16*16*1024 points)
+    ("src.fuse 1024->1024", 262144, 1024, 1024),
+    ("src.ppo0 1024->512", 262144, 512, 1024),
+    ("src.ppo3 512->512", 262144, 512, 512),
+    ("src.mlp2.6 128->1024", 262144, 1024, 128),
+    ("recon_src R1 512->256", 262144, 256, 512),
+]
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    ge.build()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    out = {}
+    for name, M, N, Kd in SHAPES:
+        X = torch.randn(M, Kd, device=dev, generator=g)
+        W = torch.randn(N, Kd, device=dev, generator=g) * 0.05
+        s = torch.rand(Kd, device=dev, generator=g) + 0.5
+        t = torch.randn(Kd, device=dev, generator=g) * 0.1
+        Y = torch.empty(M, N, device=dev)
+        ws = torch.empty(K.nblocks(M), 2, N, device=dev)
+        dY = torch.randn(M, N, device=dev, generator=g)
+        G = torch.empty(M, Kd, device=dev)
+        bws = torch.empty(K.nblocks(M), 2, Kd, device=dev)
+        st = K.BNState(torch.zeros(Kd, device=dev), torch.ones(Kd, device=dev), s, t)
+        dW = torch.empty(N, Kd, device=dev)
+        flop = 2.0 * M * N * Kd
+        r = {}
+        r["fwd"] = flop / timeit(lambda: K.gemm(M, N, Kd, X, Kd, W, Kd, Y, N, pro_a=K.PRO_ENC, pro_s=s, pro_t=t,
+                                                epi=K.EPI_FWD, stat_ws=ws), a.iters) / 1e12
+        r["fwd_store"] = flop / timeit(lambda: K.gemm(M, N, Kd, X, Kd, W, Kd, Y, N), a.iters) / 1e12
+        r["dgrad_bnbwd"] = flop / timeit(lambda: K.gemm(M, Kd, N, dY, N, W, Kd, G, Kd, b_kmajor=True, epi=K.EPI_BNBWD,
+                                                        Yp=X, ldy=Kd, bn=st, bwd_ws=bws), a.iters) / 1e12
+        r["wgrad"] = flop / timeit(lambda: K.wgrad(dY, N, X, Kd, N, Kd, M, dW, Kd, pro=K.PRO_ENC, pro_s=s, pro_t=t),
+                                   a.iters) / 1e12
+        out[name] = {k: round(v, 1) for k, v in r.items()}
+        print(name, out[name], flush=True)
+        del X, W, Y, ws, dY, G, bws, dW
+        torch.cuda.empty_cache()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
