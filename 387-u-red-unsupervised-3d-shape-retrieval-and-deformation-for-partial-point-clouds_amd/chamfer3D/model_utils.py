@@ -6,6 +6,8 @@ dist1 is gt -> output (model_utils.py:56); kept here.
 """
 import torch
 
+from ured_hip import nn as unn
+
 from .dist_chamfer_3D import chamfer_3DDist
 
 
@@ -41,6 +43,14 @@ def calc_dcd(x, gt, alpha=1000, n_lambda=1, return_raw=False, non_reg=False):
         frac_12, frac_21 = max(1, n_x / n_gt), max(1, n_gt / n_x)
     else:
         frac_12, frac_21 = n_x / n_gt, n_gt / n_x
+    if not (torch.is_grad_enabled() and (x.requires_grad or gt.requires_grad)) and n_x + n_gt <= unn.DCD_MAX_POINTS:
+        # forward-only (metrics, pseudo-labels): NN + one fused reduction kernel (ured_dcd)
+        dist1, dist2, idx1, idx2 = unn.nn_dense(gt, x)
+        loss, cd_p, cd_t = unn.dcd(dist1, idx1, dist2, idx2, alpha, n_lambda, frac_12, frac_21)
+        res = [loss, cd_p, cd_t]
+        if return_raw:
+            res.extend([dist1, dist2, idx1, idx2])
+        return res
     cd_p, cd_t, dist1, dist2, idx1, idx2 = calc_cd(x, gt, return_raw=True)
     # dist1/idx1: every gt point -> its NN in x; dist2/idx2: every x point -> its NN in gt
     exp1, exp2 = torch.exp(-dist1 * alpha), torch.exp(-dist2 * alpha)

@@ -206,7 +206,7 @@ template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; }
 #define REDI(a, q, c) red_i[((a) * 2 + (q)) * BN + (c)]
 template <int EPI>
 __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2], int m0, int n0,
-                                         float* red_f, int* red_i) {
+                                         float* red_f, int* red_i, const f16v* ypre = nullptr) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
     // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
     const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
@@ -367,6 +367,21 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
 
     if (EPI == URED_EPI_BNBWD) {
         float s1[2], s2[2];
+        // ypre (v2 kernel) holds the j = 0 half of this lane's Yp values, loaded under the last
+        // K-tile; the j = 1 half is issued here so it lands while j = 0 is processed
+        f16v y1[2];
+        if (ypre) {
+            int col = n0 + wn * 64 + 32 + (lane & 31);
+            col = col < d.N ? col : d.N - 1;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    int row = row_of(i, r);
+                    row = row < d.M ? row : d.M - 1;
+                    y1[i][r] = d.Yp[(size_t)row * d.ldy + col];
+                }
+        }
         // max-pool backward: the pooled gradient lands on the winning row of each (group, column)
         const bool pool_blk = d.pool_idx && (d.pool_group_rows % BM == 0);
         const int pg = pool_blk ? m0 / d.pool_group_rows : 0;
@@ -392,7 +407,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                         const size_t ge = (size_t)(row / d.pool_group_rows) * d.N + col;
                         if (d.pool_idx[ge] == row) dh += d.pool_grad[ge];
                     }
-                    const float y = d.Yp[(size_t)row * d.ldy + col];
+                    const float y = ypre ? (j == 0 ? ypre[i][r] : y1[i][r]) : d.Yp[(size_t)row * d.ldy + col];
                     float g, xh;
                     if (d.bwd_res) {
                         g = dh;
@@ -589,6 +604,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    f16v ypre[2];      // BN-backward epilogue operand, j = 0 half (EPI_BNBWD only; dead otherwise)
 
     // k-major B with prologue (wgrad): the channel is this lane's output column, fixed
     float bs_[2] = {1.f, 1.f}, bt_[2] = {0.f, 0.f};
@@ -614,28 +630,16 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         for (int k0 = kbeg; k0 < kend; k0 += BK) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (k0 + BK < kend) issue(stage ^ 1, k0 + BK);   // lands while this tile is multiplied
             const float* As = smem + stage * 2 * TILE;
             const float* Bs = As + TILE;
             const bool tail = k0 + BK > kend;
 
-            // ---- A fragments: a[tm][j] for k = k0 + 16h + j
-            float a[2][16];
+            // ---- every fragment of this tile goes LDS -> VGPR before the next tile's DMA is
+            // issued: the compiler orders a global_load_lds before any later ds_read with a
+            // vmcnt(0) (it cannot prove the stages disjoint), which would expose the prefetch.
+            // a[tm][j], b[tn][j] for k = k0 + 16h + j
+            float a[2][16], b[2][16];
             if constexpr (!A_KM) {
-                float as_[16], at_[16];
-                bool raw = false;
-                if (PRO_A != URED_PRO_NONE) {
-                    int kc = k0 + 16 * h;
-                    raw = kc >= d.k1;
-                    kc = raw ? d.k1 - 16 : kc;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float4 sv = *reinterpret_cast<const float4*>(d.pro_s + kc + 4 * q);
-                        const float4 tv = *reinterpret_cast<const float4*>(d.pro_t + kc + 4 * q);
-                        as_[4 * q] = sv.x; as_[4 * q + 1] = sv.y; as_[4 * q + 2] = sv.z; as_[4 * q + 3] = sv.w;
-                        at_[4 * q] = tv.x; at_[4 * q + 1] = tv.y; at_[4 * q + 2] = tv.z; at_[4 * q + 3] = tv.w;
-                    }
-                }
 #pragma unroll
                 for (int tm = 0; tm < 2; ++tm) {
                     const int r = wm * 64 + tm * 32 + li;
@@ -644,10 +648,6 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                         const float4 v = *reinterpret_cast<const float4*>(As + r * 32 + 4 * ((4 * h + q) ^ (r & 7)));
                         a[tm][4 * q] = v.x; a[tm][4 * q + 1] = v.y; a[tm][4 * q + 2] = v.z; a[tm][4 * q + 3] = v.w;
                     }
-                    if (PRO_A != URED_PRO_NONE) {
-#pragma unroll
-                        for (int j = 0; j < 16; ++j) a[tm][j] = raw ? a[tm][j] : pro_v<PRO_A>(a[tm][j], as_[j], at_[j]);
-                    }
                 }
             } else {
 #pragma unroll
@@ -655,45 +655,87 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
 #pragma unroll
                     for (int j = 0; j < 16; ++j) a[tm][j] = As[(16 * h + j) * BM + wm * 64 + tm * 32 + li];
             }
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn) {
+                const int cidx = wn * 64 + tn * 32 + li;
+                if constexpr (!B_KM) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 v = *reinterpret_cast<const float4*>(Bs + cidx * 32 + 4 * ((4 * h + q) ^ (cidx & 7)));
+                        b[tn][4 * q] = v.x; b[tn][4 * q + 1] = v.y; b[tn][4 * q + 2] = v.z; b[tn][4 * q + 3] = v.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) b[tn][j] = Bs[(16 * h + j) * BN + cidx];
+                }
+            }
+            // the prologue's per-channel scale/shift: global loads issued BEFORE the DMA, so
+            // waiting for them (vmcnt counts in order) does not wait for the next tile
+            float ss[16], tt[16];
+            bool raw = false;
+            if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
+                int kc = k0 + 16 * h;
+                raw = kc >= d.k1;
+                kc = raw ? d.k1 - 16 : kc;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 sv = *reinterpret_cast<const float4*>(d.pro_s + kc + 4 * q);
+                    const float4 tv = *reinterpret_cast<const float4*>(d.pro_t + kc + 4 * q);
+                    ss[4 * q] = sv.x; ss[4 * q + 1] = sv.y; ss[4 * q + 2] = sv.z; ss[4 * q + 3] = sv.w;
+                    tt[4 * q] = tv.x; tt[4 * q + 1] = tv.y; tt[4 * q + 2] = tv.z; tt[4 * q + 3] = tv.w;
+                }
+            }
+            if (k0 + BK < kend) {
+                issue(stage ^ 1, k0 + BK);   // lands while this tile is multiplied
+            } else if constexpr (EPI == URED_EPI_BNBWD) {
+                // last tile: the BN-backward epilogue's Yp tile streams in under its MFMAs
+                int col = n0 + wn * 64 + li;
+                col = col < d.N ? col : d.N - 1;
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        int row = m0 + wm * 64 + 4 * h + i * 32 + (r & 3) + 8 * (r >> 2);
+                        row = row < d.M ? row : d.M - 1;
+                        ypre[i][r] = d.Yp[(size_t)row * d.ldy + col];
+                    }
+            }
+
+            // ---- prologues (previous layer's BN+ReLU) and the K tail, on the fragments
+            if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int tm = 0; tm < 2; ++tm)
+                            a[tm][4 * q + e] = raw ? a[tm][4 * q + e] : pro_v<PRO_A>(a[tm][4 * q + e], ss[4 * q + e], tt[4 * q + e]);
+            }
+            if constexpr (B_KM && PRO_B != URED_PRO_NONE) {
+#pragma unroll
+                for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) b[tn][j] = pro_v<PRO_B>(b[tn][j], bs_[tn], bt_[tn]);
+            }
             if (tail) {   // zero the k >= K part of the reduction (the images hold clamped copies)
 #pragma unroll
                 for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
                     for (int j = 0; j < 16; ++j) a[tm][j] = (k0 + 16 * h + j < kend) ? a[tm][j] : 0.f;
             }
-            // ---- B fragments + MFMAs
+            // ---- MFMAs
 #pragma unroll
-            for (int jq = 0; jq < 4; ++jq) {
-                float b[2][4];
-#pragma unroll
-                for (int tn = 0; tn < 2; ++tn) {
-                    const int cidx = wn * 64 + tn * 32 + li;
-                    if constexpr (!B_KM) {
-                        const float4 v = *reinterpret_cast<const float4*>(Bs + cidx * 32 + 4 * ((4 * h + jq) ^ (cidx & 7)));
-                        b[tn][0] = v.x; b[tn][1] = v.y; b[tn][2] = v.z; b[tn][3] = v.w;
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            float x = Bs[(16 * h + 4 * jq + e) * BN + cidx];
-                            if (PRO_B != URED_PRO_NONE) x = pro_v<PRO_B>(x, bs_[tn], bt_[tn]);
-                            b[tn][e] = x;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int j = 4 * jq + e;
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[0][e], acc[0][0], 0, 0, 0);
-                    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[1][e], acc[0][1], 0, 0, 0);
-                    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[0][e], acc[1][0], 0, 0, 0);
-                    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][e], acc[1][1], 0, 0, 0);
-                }
+            for (int j = 0; j < 16; ++j) {
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[0][j], acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[1][j], acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[0][j], acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][j], acc[1][1], 0, 0, 0);
             }
             stage ^= 1;
         }
         __syncthreads();   // all waves done with the stages before the epilogue reuses LDS
     }
-    epilogue<EPI>(d, acc, m0, n0, red_f, red_i);
+    epilogue<EPI>(d, acc, m0, n0, red_f, red_i, EPI == URED_EPI_BNBWD && kbeg < kend ? ypre : nullptr);
 }
 
 // ---- small kernels -------------------------------------------------------------
@@ -803,6 +845,56 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
         s += v;
     }
     if (colsum) colsum[(size_t)blk * N + n] = s;
+}
+
+// float4 form (N, ld multiples of 4, 16-B aligned bases): block = 64 column quads x 4 row
+// lanes; lane row ty walks rows r0+ty, r0+ty+4, ... so every row read is 1 KB contiguous per
+// wave, 8 rows in flight per lane; the 4 row lanes' column sums combine in LDS in fixed order.
+__global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restrict__ G, const float* __restrict__ Y,
+        int M, int N, int ld, int res, const float* __restrict__ mean, const float* __restrict__ ca,
+        const float* __restrict__ cb, const float* __restrict__ cc, float* __restrict__ dY, float* __restrict__ colsum) {
+    __shared__ float4 part[4][64];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int n = (blockIdx.x * 64 + tx) * 4;
+    const int blk = blockIdx.y;
+    const bool nv = n < N;
+    const int nn = nv ? n : 0;
+    const float4 a = *reinterpret_cast<const float4*>(ca + nn), b = *reinterpret_cast<const float4*>(cb + nn);
+    const float4 c = *reinterpret_cast<const float4*>(cc + nn), mu = *reinterpret_cast<const float4*>(mean + nn);
+    const int r0 = blk * BM, r1 = min(M, r0 + BM);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto one = [&](float y, float g, float av, float bv, float cv, float m) {
+        const float p = res ? fmaxf(y, 0.f) : y;
+        float v = __builtin_fmaf(av, g, __builtin_fmaf(bv, p - m, cv));
+        return (res && !(y > 0.f)) ? 0.f : v;
+    };
+    if (nv) {
+#pragma unroll 8
+        for (int r = r0 + ty; r < r1; r += 4) {
+            const size_t e = (size_t)r * ld + n;
+            const float4 y = *reinterpret_cast<const float4*>(Y + e);
+            const float4 g = *reinterpret_cast<const float4*>(G + e);
+            float4 v;
+            v.x = one(y.x, g.x, a.x, b.x, c.x, mu.x);
+            v.y = one(y.y, g.y, a.y, b.y, c.y, mu.y);
+            v.z = one(y.z, g.z, a.z, b.z, c.z, mu.z);
+            v.w = one(y.w, g.w, a.w, b.w, c.w, mu.w);
+            *reinterpret_cast<float4*>(dY + e) = v;
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+    }
+    if (!colsum) return;
+    part[ty][tx] = s;
+    __syncthreads();
+    if (ty == 0 && nv) {
+        float4 t = part[0][tx];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            const float4 u = part[q][tx];
+            t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        }
+        *reinterpret_cast<float4*>(colsum + (size_t)blk * N + n) = t;
+    }
 }
 
 __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restrict__ ws, int M, int N, int group_rows,
@@ -1001,9 +1093,17 @@ int ured_bn_bwd_apply(const float* G, const float* Y, int M, int N, int ld, int 
     URED_REQUIRE(M >= 0 && N >= 0 && ld >= N, "ured_bn_bwd_apply: bad sizes");
     if (M == 0 || N == 0) return 0;
     URED_REQUIRE(G && Y && mean && coef_a && coef_b && coef_c && dY, "ured_bn_bwd_apply: null pointer");
-    dim3 grid((N + 255) / 256, (M + BM - 1) / BM);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(256), 0, (hipStream_t)stream, G, Y, M, N, ld, res, mean,
-                       coef_a, coef_b, coef_c, dY, colsum_ws);
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (N % 4 == 0 && ld % 4 == 0 && al16(G) && al16(Y) && al16(dY) && al16(mean) && al16(coef_a) &&
+        al16(coef_b) && al16(coef_c) && (!colsum_ws || al16(colsum_ws))) {
+        dim3 grid((N / 4 + 63) / 64, (M + BM - 1) / BM);
+        hipLaunchKernelGGL(bn_bwd_apply4_kernel, grid, dim3(256), 0, (hipStream_t)stream, G, Y, M, N, ld, res, mean,
+                           coef_a, coef_b, coef_c, dY, colsum_ws);
+    } else {
+        dim3 grid((N + 255) / 256, (M + BM - 1) / BM);
+        hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(256), 0, (hipStream_t)stream, G, Y, M, N, ld, res, mean,
+                           coef_a, coef_b, coef_c, dY, colsum_ws);
+    }
     return ured::launch_status("ured_bn_bwd_apply");
 }
 

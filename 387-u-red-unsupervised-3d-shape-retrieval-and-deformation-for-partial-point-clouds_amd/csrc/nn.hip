@@ -21,8 +21,9 @@
 //     the ref range when there are too few queries to fill 256 CUs, merged in
 //     LDS by (value, chunk) lexicographic min (order-independent result).
 // Backward: gather form, deterministic (no float atomics): each point owns its
-//   output; the contributions of the other direction are found by scanning the
-//   other side's idx array through LDS in ascending order.
+//   output; the contributions of the other direction are found by streaming the
+//   other side's idx array through LDS in ascending order, each wave compacting
+//   the entries that target its own 64 points (O(n + m) work per pair).
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -190,6 +191,7 @@ struct NNBwdArgs {
 __global__ __launch_bounds__(NN_THREADS) void nn_bwd_kernel(NNBwdArgs args) {
     __shared__ __attribute__((aligned(16))) int sidx[NN_TILE];
     __shared__ float sg[NN_TILE], sx[NN_TILE], sy[NN_TILE], sz[NN_TILE];
+    __shared__ int slist[(NN_THREADS / 64) * NN_TILE];   // per-wave compacted entry lists
     const int dir = blockIdx.z, s = blockIdx.y;
     int ao, al, bo, bl;
     if (args.segs) { int4 q = args.segs[s]; ao = q.x; al = q.y; bo = q.z; bl = q.w; }
@@ -226,22 +228,31 @@ __global__ __launch_bounds__(NN_THREADS) void nn_bwd_kernel(NNBwdArgs args) {
                 sidx[i] = id; sg[i] = gg; sx[i] = x; sy[i] = y; sz[i] = z;
             }
             __syncthreads();
-            const int4* si4 = reinterpret_cast<const int4*>(sidx);
-            for (int k4 = 0; k4 < (tn + 3) / 4; ++k4) {
-                const int4 ii = si4[k4];
-                const bool hit = (ii.x == j) | (ii.y == j) | (ii.z == j) | (ii.w == j);
-                if (hit) {
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) {
-                        const int k = 4 * k4 + w;
-                        if (sidx[k] == j) {
-                            const float g = sg[k] * 2.f;
-                            ax = ax - g * (sx[k] - px);
-                            ay = ay - g * (sy[k] - py);
-                            az = az - g * (sz[k] - pz);
-                        }
-                    }
-                }
+            // Each wave compacts, in ascending k, the tile entries whose NN lands in its own 64
+            // points (ballot + prefix popcount), then walks only that list; the owner lane
+            // accumulates. Same summation order as a full ascending scan (own term first, then
+            // k ascending), so the result is bit-identical to it — without every lane paying
+            // for every entry.
+            const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+            const int jw0 = j0 + wv * 64;
+            int* lst = slist + wv * NN_TILE;
+            int cnt = 0;
+            for (int c = 0; c < tn; c += 64) {
+                const int k = c + ln;
+                const int id = k < tn ? sidx[k] : -1;
+                const bool pred = (unsigned)(id - jw0) < 64u;
+                const unsigned long long mask = __ballot(pred);
+                if (pred) lst[cnt + __popcll(mask & ((1ull << ln) - 1ull))] = k;
+                cnt += __popcll(mask);
+            }
+            for (int e = 0; e < cnt; ++e) {
+                const int k = lst[e];
+                const bool own = sidx[k] == j;
+                const float g = sg[k] * 2.f;
+                const float nx = ax - g * (sx[k] - px);
+                const float ny = ay - g * (sy[k] - py);
+                const float nz = az - g * (sz[k] - pz);
+                ax = own ? nx : ax; ay = own ? ny : ay; az = own ? nz : az;
             }
         }
     }
@@ -280,6 +291,64 @@ int bwd_dispatch(const NNBwdArgs& a, int nseg, int max_a, int max_b, hipStream_t
     dim3 grid((max_p + NN_THREADS - 1) / NN_THREADS, nseg, 2);
     hipLaunchKernelGGL(nn_bwd_kernel, grid, dim3(NN_THREADS), 0, st, a);
     return 0;
+}
+
+
+// ---- density-aware chamfer reduction (calc_dcd, utils_v2/model_utils.py:13-51) --------
+// One workgroup per batch item. NN visit counts live in LDS (integer atomics: exact), the
+// six per-item sums are strided per thread then tree-reduced in a fixed order.
+constexpr int DCD_THREADS = 256;
+constexpr int DCD_MAX_POINTS = 16384;   // n1 + n2 per item (64 KiB of LDS counts)
+
+__global__ __launch_bounds__(DCD_THREADS) void dcd_kernel(const float* __restrict__ d1, const int* __restrict__ i1,
+        const float* __restrict__ d2, const int* __restrict__ i2, int n1, int n2, float alpha, int lam,
+        float frac12, float frac21, float* __restrict__ loss, float* __restrict__ cdp, float* __restrict__ cdt) {
+    extern __shared__ int cnt[];            // [n2] visits of x points by gt NNs, then [n1] vice versa
+    __shared__ float red[6][DCD_THREADS];
+    int* c1 = cnt;                           // indexed by idx1 (an x point)
+    int* c2 = cnt + n2;                      // indexed by idx2 (a gt point)
+    const int b = blockIdx.x, t = threadIdx.x;
+    const float* D1 = d1 + (size_t)b * n1; const int* I1 = i1 + (size_t)b * n1;
+    const float* D2 = d2 + (size_t)b * n2; const int* I2 = i2 + (size_t)b * n2;
+    for (int k = t; k < n1 + n2; k += DCD_THREADS) cnt[k] = 0;
+    __syncthreads();
+    for (int k = t; k < n1; k += DCD_THREADS) atomicAdd(&c1[I1[k]], 1);
+    for (int k = t; k < n2; k += DCD_THREADS) atomicAdd(&c2[I2[k]], 1);
+    __syncthreads();
+    auto wpow = [&](int c) {
+        const float f = (float)c;
+        return lam == 1 ? f : (lam == 2 ? f * f : powf(f, (float)lam));
+    };
+    float l1 = 0.f, l2 = 0.f, s1 = 0.f, s2 = 0.f, t1 = 0.f, t2 = 0.f;
+    for (int k = t; k < n1; k += DCD_THREADS) {
+        const float d = D1[k];
+        const float w = (1.0f / (wpow(c1[I1[k]]) + 1e-6f)) * frac21;
+        l1 += 1.0f - expf(-d * alpha) * w;
+        s1 += sqrtf(d);
+        t1 += d;
+    }
+    for (int k = t; k < n2; k += DCD_THREADS) {
+        const float d = D2[k];
+        const float w = (1.0f / (wpow(c2[I2[k]]) + 1e-6f)) * frac12;
+        l2 += 1.0f - expf(-d * alpha) * w;
+        s2 += sqrtf(d);
+        t2 += d;
+    }
+    red[0][t] = l1; red[1][t] = l2; red[2][t] = s1; red[3][t] = s2; red[4][t] = t1; red[5][t] = t2;
+    __syncthreads();
+    for (int h = DCD_THREADS / 2; h > 0; h >>= 1) {
+        if (t < h) {
+#pragma unroll
+            for (int q = 0; q < 6; ++q) red[q][t] += red[q][t + h];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const float fn1 = (float)n1, fn2 = (float)n2;
+        loss[b] = (red[0][0] / fn1 + red[1][0] / fn2) / 2.0f;
+        cdp[b] = (red[2][0] / fn1 + red[3][0] / fn2) / 2.0f;
+        cdt[b] = red[4][0] / fn1 + red[5][0] / fn2;
+    }
 }
 
 }  // namespace
@@ -343,6 +412,20 @@ int ured_nn_seg_bwd(const float* a, const float* b, const int* segs, int nseg,
     NNBwdArgs A{a, b, reinterpret_cast<const int4*>(segs), 0, 0, gd_a, gd_b, idx_a, idx_b, ga, gb};
     bwd_dispatch(A, nseg, max_a_len, max_b_len, (hipStream_t)stream);
     return ured::launch_status("ured_nn_seg_bwd");
+}
+
+int ured_dcd(const float* dist1, const int* idx1, const float* dist2, const int* idx2, int b, int n1, int n2,
+             float alpha, int n_lambda, float frac_12, float frac_21, float* loss, float* cd_p, float* cd_t,
+             void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(b >= 0 && n1 > 0 && n2 > 0, "ured_dcd: bad sizes b=%d n1=%d n2=%d", b, n1, n2);
+    URED_REQUIRE(n1 + n2 <= DCD_MAX_POINTS, "ured_dcd: n1+n2=%d exceeds %d", n1 + n2, DCD_MAX_POINTS);
+    URED_REQUIRE(n_lambda >= 0, "ured_dcd: n_lambda must be >= 0");
+    if (b == 0) return 0;
+    URED_REQUIRE(dist1 && idx1 && dist2 && idx2 && loss && cd_p && cd_t, "ured_dcd: null pointer");
+    hipLaunchKernelGGL(dcd_kernel, dim3(b), dim3(DCD_THREADS), (size_t)(n1 + n2) * sizeof(int), (hipStream_t)stream,
+                       dist1, idx1, dist2, idx2, n1, n2, alpha, n_lambda, frac_12, frac_21, loss, cd_p, cd_t);
+    return ured::launch_status("ured_dcd");
 }
 
 }  // extern "C"

@@ -17,6 +17,7 @@ ABI_VERSION = 1
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
+_F = ctypes.c_float
 
 # name -> argtypes (all functions return int status, 0 = ok)
 _SIGNATURES = {
@@ -24,6 +25,7 @@ _SIGNATURES = {
     "ured_nn_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "ured_nn_seg_fwd": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_nn_seg_bwd": [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "ured_dcd": [_P, _P, _P, _P, _I, _I, _I, _F, _I, _F, _F, _P, _P, _P, _P],
 }
 
 _lib = None

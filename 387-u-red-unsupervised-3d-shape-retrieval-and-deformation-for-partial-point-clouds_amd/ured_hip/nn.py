@@ -124,3 +124,24 @@ def nn_segments(a, b, segs, max_a, max_b, dirs=3):
     a_shape, b_shape = a.shape[:-1], b.shape[:-1]
     da, ia, db, ib = NNSegFunction.apply(a.reshape(-1, 3), b.reshape(-1, 3), segs, max_a, max_b, dirs)
     return da.view(a_shape), ia.view(a_shape), db.view(b_shape), ib.view(b_shape)
+
+
+DCD_MAX_POINTS = 16384
+
+
+def dcd(dist1, idx1, dist2, idx2, alpha=1000.0, n_lambda=1, frac_12=None, frac_21=None):
+    """Fused density-aware chamfer tail (calc_dcd, utils_v2/model_utils.py:13-51) on dense NN
+    outputs: dist1/idx1 [b,n1] gt -> x, dist2/idx2 [b,n2] x -> gt (from nn_dense(gt, x)).
+    Returns (loss [b], cd_p [b], cd_t [b]); forward only."""
+    b, n1 = dist1.shape
+    n2 = dist2.shape[1]
+    frac_12 = n2 / n1 if frac_12 is None else frac_12
+    frac_21 = n1 / n2 if frac_21 is None else frac_21
+    _lib.require_device(dist1, dist2)
+    dist1, dist2 = dist1.contiguous(), dist2.contiguous()
+    idx1, idx2 = idx1.to(torch.int32).contiguous(), idx2.to(torch.int32).contiguous()
+    out = torch.empty(3, b, device=dist1.device, dtype=torch.float32)
+    _lib.call("ured_dcd", _lib.ptr(dist1), _lib.ptr(idx1), _lib.ptr(dist2), _lib.ptr(idx2), b, n1, n2,
+              float(alpha), int(n_lambda), float(frac_12), float(frac_21),
+              _lib.ptr(out[0]), _lib.ptr(out[1]), _lib.ptr(out[2]), _lib.stream_of(dist1))
+    return out[0], out[1], out[2]

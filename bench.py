@@ -79,6 +79,17 @@ class GemmTimer:
             d["bytes"] += 4.0 * (M * K + K * N + M * N) + extra
         return by
 
+    def shapes(self):
+        torch.cuda.synchronize()
+        by = {}
+        for epi, ak, bk, pa, pb, M, N, K, e0, e1 in self.rec:
+            key = f"epi{epi} akm{int(bool(ak))} bkm{int(bool(bk))} pa{pa} pb{pb} M{M} N{N} K{K}"
+            d = by.setdefault(key, {"launches": 0, "ms": 0.0})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["tflops"] = round(2.0 * M * N * K * d["launches"] / (d["ms"] * 1e-3) / 1e12, 1)
+        return dict(sorted(by.items(), key=lambda kv: -kv[1]["ms"]))
+
 
 def cpu_baseline(args, cfg_small_threads=16):
     """The oracle (CPU restatement, torch fp32) timed on this host on a bounded sample."""
@@ -141,6 +152,7 @@ def main():
     ap.add_argument("--sources", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true")
+    ap.add_argument("--shapes-out", default=None, help="write the per-shape GEMM breakdown (JSON) here")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +201,9 @@ def main():
         with GemmTimer() as gt:
             step.step(batches[0])
         breakdown = gt.summary()
+        if args.shapes_out and rank == 0:
+            with open(args.shapes_out, "w") as f:
+                json.dump(gt.shapes(), f, indent=1)
 
     if rank != 0:
         if world > 1:

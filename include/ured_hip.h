@@ -78,6 +78,19 @@ int ured_nn_seg_bwd(const float* a, const float* b, const int* segs, int nseg,
                     float* ga, float* gb, void* stream);
 
 
+/* Density-aware chamfer reduction of dense NN outputs (replaces the torch tail of
+ * calc_dcd, Density_aware_Chamfer_Distance/utils_v2/model_utils.py:13-51, and the
+ * cd_p / cd_t of calc_cd, :53-70; the NN itself is ured_nn_fwd with xyz1 = gt,
+ * xyz2 = x, as calc_cd calls cham_loss(gt, output)).
+ * dist1/idx1 [b,n1]: gt -> x; dist2/idx2 [b,n2]: x -> gt. Per item:
+ *   w1 = frac_21 / (count_x(idx1)^n_lambda + 1e-6),  loss1 = mean(1 - exp(-alpha d1) w1)
+ *   w2 = frac_12 / (count_gt(idx2)^n_lambda + 1e-6), loss2 = mean(1 - exp(-alpha d2) w2)
+ *   loss = (loss1 + loss2)/2, cd_p = (mean sqrt d1 + mean sqrt d2)/2, cd_t = mean d1 + mean d2.
+ * Forward only (no autograd), deterministic. n1 + n2 <= 16384. */
+int ured_dcd(const float* dist1, const int* idx1, const float* dist2, const int* idx2, int b, int n1, int n2,
+             float alpha, int n_lambda, float frac_12, float frac_21, float* loss, float* cd_p, float* cd_t,
+             void* stream);
+
 /* ---------------- per-point MLP (1x1 conv) on fp32 MFMA ---------------- *
  * Replaces the Conv1d(k=1)+BatchNorm1d+ReLU chains of TargetEncoder
  * (network/simple_encoder.py:52-107) and re_residual_net / FeedForwardNet_norm

@@ -75,6 +75,24 @@ def test_dense_bwd(unn, dev, b, n, m):
     assert torch.equal(a2.grad, a.grad)
 
 
+@pytest.mark.parametrize("n,m", [(3000, 5), (5000, 1), (70, 1300)])
+def test_dense_bwd_degenerate(unn, dev, n, m):
+    """Many queries sharing one NN (long per-point contribution lists, > one LDS tile)."""
+    p1 = _rand((2, n, 3), 21)
+    p2 = np.repeat(_rand((2, 1, 3), 22), m, axis=1).copy()   # m identical refs -> all map to index 0
+    g1, g2 = _rand((2, n), 23) - 0.5, _rand((2, m), 24) - 0.5
+    a = torch.from_numpy(p1).to(dev).requires_grad_(True)
+    c = torch.from_numpy(p2).to(dev).requires_grad_(True)
+    d1, d2, i1, i2 = unn.nn_dense(a, c)
+    (d1 * torch.from_numpy(g1).to(dev)).sum().add((d2 * torch.from_numpy(g2).to(dev)).sum()).backward()
+    r = nn_ref.nn_fwd(p1, p2)
+    np.testing.assert_array_equal(i1.cpu().numpy(), r[2])
+    ga, gc = nn_ref.nn_bwd(p1, p2, g1, g2, r[2], r[3])
+    np.testing.assert_allclose(a.grad.cpu().numpy(), ga, rtol=1e-6, atol=1e-7)
+    # up to 5000 terms summed in a different order from the scatter-form oracle
+    np.testing.assert_allclose(c.grad.cpu().numpy(), gc, rtol=1e-5, atol=1e-3)
+
+
 def _segs(rng, na_tot, nb_tot, nseg, max_a, max_b, allow_empty=True):
     segs, ao, bo = [], 0, 0
     for _ in range(nseg):

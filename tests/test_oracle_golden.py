@@ -175,3 +175,47 @@ def test_train_step_golden():
                                g["g/recon_src.9.weight"], rtol=2e-3, atol=1e-5)
     np.testing.assert_allclose(P["re_residual_net_full"]["residual_net.9.weight"].grad.numpy(),
                                g["g/re_res.9.weight"], rtol=2e-3, atol=1e-5)
+
+
+def test_dcd_oracle_vs_reference_golden():
+    """oracle.dcd_ref.calc_dcd vs the reference's calc_dcd (model_utils.py:13-51) run on the
+    reference's float64 distChamfer (tests/golden/make_golden.py golden_dcd)."""
+    from oracle import dcd_ref
+    g = _g("dcd.npz")
+    for name in ("r3x300x200", "r2x1024x1024", "r4x64x512"):
+        x, gt = g[name + "/x"], g[name + "/gt"]
+        for nr in (0, 1):
+            loss, cd_p, cd_t = dcd_ref.calc_dcd(x, gt, non_reg=bool(nr))
+            tag = f"{name}/nr{nr}"
+            np.testing.assert_allclose(loss, g[tag + "/loss"], rtol=0, atol=2e-6)
+            np.testing.assert_allclose(cd_p, g[tag + "/cd_p"], rtol=0, atol=2e-6)
+            np.testing.assert_allclose(cd_t, g[tag + "/cd_t"], rtol=0, atol=2e-6)
+        loss, _, _ = dcd_ref.calc_dcd(x, gt, alpha=200, n_lambda=2)
+        np.testing.assert_allclose(loss, g[name + "/a200l2/loss"], rtol=0, atol=2e-6)
+
+
+def test_pair_rows_connect_matrix():
+    """get_src_pair rows + sources_connect composition (symmetric, diagonal doubled)."""
+    from oracle import dcd_ref
+    pts = np.random.Generator(np.random.PCG64(3)).random((5, 64, 3), dtype=np.float32)
+    rows = dcd_ref.pair_rows(pts)
+    assert [len(rows[i][0]) for i in range(5)] == [5, 4, 3, 2, 1]
+    m = dcd_ref.connect_matrix(rows, 5)
+    np.testing.assert_array_equal(m, m.transpose(0, 2, 1))
+    d, _, _ = dcd_ref.calc_dcd(pts[3:4], pts[1:2])
+    assert m[0, 1, 3] == np.float64(d[0])
+    assert m[2, 2, 2] == 0.0 and abs(m[0, 2, 2] - 2e-6) < 1e-7   # self pair: dcd = 1 - 1/(1+1e-6)
+
+
+def test_shard_rows_balanced_and_complete():
+    import sys
+    from conftest import PKG_DIR
+    sys.path.insert(0, PKG_DIR)
+    from engine.generate_pair import shard_rows
+    for n in (1, 2, 7, 100, 513):
+        for world in (1, 2, 3, 8):
+            shards = [shard_rows(n, r, world) for r in range(world)]
+            assert sorted(sum(shards, [])) == list(range(n))
+            loads = [sum(n - i for i in s) for s in shards]
+            if n >= 8 * world:
+                assert max(loads) - min(loads) <= n + 1, (n, world, loads)   # at most one zig-zag pair

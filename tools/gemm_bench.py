@@ -64,6 +64,10 @@ def main():
         r["fwd"] = flop / timeit(lambda: K.gemm(M, N, Kd, X, Kd, W, Kd, Y, N, pro_a=K.PRO_ENC, pro_s=s, pro_t=t,
                                                 epi=K.EPI_FWD, stat_ws=ws), a.iters) / 1e12
         r["fwd_store"] = flop / timeit(lambda: K.gemm(M, N, Kd, X, Kd, W, Kd, Y, N), a.iters) / 1e12
+        r["pro_store"] = flop / timeit(lambda: K.gemm(M, N, Kd, X, Kd, W, Kd, Y, N, pro_a=K.PRO_ENC, pro_s=s,
+                                                      pro_t=t), a.iters) / 1e12
+        r["stats_nopro"] = flop / timeit(lambda: K.gemm(M, N, Kd, X, Kd, W, Kd, Y, N, epi=K.EPI_FWD, stat_ws=ws),
+                                         a.iters) / 1e12
         r["dgrad_bnbwd"] = flop / timeit(lambda: K.gemm(M, Kd, N, dY, N, W, Kd, G, Kd, b_kmajor=True, epi=K.EPI_BNBWD,
                                                         Yp=X, ldy=Kd, bn=st, bwd_ws=bws), a.iters) / 1e12
         r["wgrad"] = flop / timeit(lambda: K.wgrad(dY, N, X, Kd, N, Kd, M, dW, Kd, pro=K.PRO_ENC, pro_s=s, pro_t=t),
