@@ -570,6 +570,56 @@ __device__ __forceinline__ void dma_tile(const float* __restrict__ G, int ld, in
     }
 }
 
+// Buffer-descriptor form of dma_tile (operands < 2 GiB, no A2 concat): the per-lane byte
+// offsets are computed once per block; a tile only adds its k offset (one VALU add per
+// DMA instead of the clamp/select/64-bit address chain). Lanes whose row (row-major) or
+// column (k-major) is outside the operand get an offset past num_records, and so does any
+// k >= K row of a k-major operand: the hardware returns zeros for them.
+constexpr unsigned BUF_OOB = 0x80000000u;
+constexpr int PRO_LDS = 1024;            // max prologue channels staged in LDS by gemm2
+constexpr int BUF_DWORD3 = 0x00020000;   // raw buffer, gfx9 family (gfx950)
+
+__host__ __device__ constexpr bool buf_only_variant(bool b_km, int epi) {
+    return b_km || epi == URED_EPI_BNBWD || epi == URED_EPI_SPLITK;   // A2 concat only feeds forward layers
+}
+__host__ __device__ inline bool buf_ok(const UredGemmDesc& d) {
+    return d.k1 >= d.K &&
+        (d.a_kmajor ? (long long)d.K * d.lda : (long long)d.M * d.lda) * 4 < 0x7fffffffLL &&
+        (d.b_kmajor ? (long long)d.K * d.ldb : (long long)d.N * d.ldb) * 4 < 0x7fffffffLL;
+}
+
+struct BufOperand {
+    __amdgpu_buffer_rsrc_t rsrc;
+    unsigned vo[4];
+};
+
+template <bool KM>
+__device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld, int ext, int e0, int K, int w, int lane) {
+    const long long bytes = KM ? ((long long)(K - 1) * ld + ext) * 4 : ((long long)(ext - 1) * ld + K) * 4;
+    o.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)bytes, BUF_DWORD3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = (w * 4 + i) * 64 + lane;
+        if constexpr (!KM) {
+            const int r = c >> 3, p = c & 7, sl = p ^ (r & 7);
+            const int row = e0 + r;
+            o.vo[i] = row < ext ? (unsigned)(((long long)row * ld + 4 * sl) * 4) : BUF_OOB;
+        } else {
+            const int kk = c >> 5, c4 = c & 31;
+            const int col = e0 + 4 * c4;
+            o.vo[i] = col < ext ? (unsigned)(((long long)kk * ld + col) * 4) : BUF_OOB;
+        }
+    }
+}
+
+template <bool KM>
+__device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, float* S, int w) {
+    const unsigned toff = KM ? (unsigned)k0 * (unsigned)ld * 4u : (unsigned)k0 * 4u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(o.rsrc, (lds_void_t*)(S + (w * 4 + i) * 256), 16, o.vo[i] + toff, 0, 0, 0);
+}
+
 template <int PRO>
 __device__ __forceinline__ float pro_v(float x, float s, float t) {
     if (PRO == URED_PRO_ENC) return fmaxf(__builtin_fmaf(x, s, t), 0.f);
@@ -580,8 +630,13 @@ __device__ __forceinline__ float pro_v(float x, float s, float t) {
 template <bool A_KM, bool B_KM, int PRO_A, int PRO_B, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     constexpr int TILE = BM * BK;                  // floats per operand image
-    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * TILE + 4 * BN];
+    // row-major A with a prologue: the per-channel scale/shift vectors (k < k1 <= PRO_LDS)
+    // are staged in LDS once, so a tile reads them with broadcast ds_reads instead of
+    // waiting on global (L2) latency every K-step
+    constexpr bool PRO_IN_LDS = !A_KM && PRO_A != URED_PRO_NONE;
+    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * TILE + 4 * BN + (PRO_IN_LDS ? 2 * PRO_LDS : 0)];
     float* red_f = smem + 4 * TILE;                // epilogue scratch (after the stages are drained)
+    float* pro_lds = smem + 4 * TILE + 4 * BN;     // [PRO_LDS] scale, [PRO_LDS] shift
     int* red_i = reinterpret_cast<int*>(smem);     // pool scratch reuses stage 0 (drained by then)
 
     const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
@@ -617,13 +672,31 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         }
     }
 
+    // operand bytes < 2 GiB and no concatenated second A source: buffer-descriptor DMA
+    // (variants that never take an A2 are launched only when buf_ok holds, see launch())
+    constexpr bool ONLY_BUF = buf_only_variant(B_KM, EPI);
+    const bool use_buf = ONLY_BUF || buf_ok(d);
+    BufOperand ba, bb;
+    if (use_buf) {
+        // a k-major operand's rows past kend must read as zero too (split-K: kend < K)
+        buf_setup<A_KM>(ba, d.A, d.lda, d.M, m0, kend, w, lane);
+        buf_setup<B_KM>(bb, d.B, d.ldb, d.N, n0, kend, w, lane);
+    }
     auto issue = [&](int stage, int k0) {
         float* As = smem + stage * 2 * TILE;
         float* Bs = As + TILE;
-        dma_tile<A_KM>(d.A, d.lda, d.M, m0, kend, k0, d.A2, d.lda2, d.k1, As, w, lane);
-        dma_tile<B_KM>(d.B, d.ldb, d.N, n0, kend, k0, d.B, 0, 0x7fffffff, Bs, w, lane);
+        if (ONLY_BUF || use_buf) {
+            buf_tile<A_KM>(ba, d.lda, k0, As, w);
+            buf_tile<B_KM>(bb, d.ldb, k0, Bs, w);
+        } else if constexpr (!ONLY_BUF) {
+            dma_tile<A_KM>(d.A, d.lda, d.M, m0, kend, k0, d.A2, d.lda2, d.k1, As, w, lane);
+            dma_tile<B_KM>(d.B, d.ldb, d.N, n0, kend, k0, d.B, 0, 0x7fffffff, Bs, w, lane);
+        }
     };
 
+    if constexpr (PRO_IN_LDS) {   // visible after the first loop barrier
+        for (int i = t; i < d.k1; i += NT) { pro_lds[i] = d.pro_s[i]; pro_lds[PRO_LDS + i] = d.pro_t[i]; }
+    }
     if (kbeg < kend) {
         issue(0, kbeg);
         int stage = 0;
@@ -673,14 +746,14 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             // waiting for them (vmcnt counts in order) does not wait for the next tile
             float ss[16], tt[16];
             bool raw = false;
-            if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
+            if constexpr (PRO_IN_LDS) {
                 int kc = k0 + 16 * h;
                 raw = kc >= d.k1;
                 kc = raw ? d.k1 - 16 : kc;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const float4 sv = *reinterpret_cast<const float4*>(d.pro_s + kc + 4 * q);
-                    const float4 tv = *reinterpret_cast<const float4*>(d.pro_t + kc + 4 * q);
+                    const float4 sv = *reinterpret_cast<const float4*>(pro_lds + kc + 4 * q);
+                    const float4 tv = *reinterpret_cast<const float4*>(pro_lds + PRO_LDS + kc + 4 * q);
                     ss[4 * q] = sv.x; ss[4 * q + 1] = sv.y; ss[4 * q + 2] = sv.z; ss[4 * q + 3] = sv.w;
                     tt[4 * q] = tv.x; tt[4 * q + 1] = tv.y; tt[4 * q + 2] = tv.z; tt[4 * q + 3] = tv.w;
                 }
@@ -974,6 +1047,7 @@ bool v2_enabled() {
 bool v2_ok(const UredGemmDesc& d) {
     if (!v2_enabled()) return false;
     if (d.pro_a && (d.k1 % 16 != 0)) return false;
+    if (d.pro_a && !d.a_kmajor && d.k1 > PRO_LDS) return false;
     if (d.K < 4 || (d.a_kmajor && d.M < 4) || (d.b_kmajor && d.N < 4)) return false;
     return true;
 }
@@ -982,7 +1056,8 @@ template <bool A_KM, bool B_KM, int PA, int PB, int EPI>
 void launch(const UredGemmDesc& d, hipStream_t st) {
     const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
     dim3 grid(ntm * ntn, 1, EPI == URED_EPI_SPLITK ? d.splits : 1);
-    if (vec_ok(d) && v2_ok(d)) hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI>), grid, dim3(NT), 0, st, d);
+    if (vec_ok(d) && v2_ok(d) && (!buf_only_variant(B_KM, EPI) || buf_ok(d)))
+        hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI>), grid, dim3(NT), 0, st, d);
     else if (vec_ok(d)) hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, true>), grid, dim3(NT), 0, st, d);
     else hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, false>), grid, dim3(NT), 0, st, d);
 }

@@ -141,6 +141,23 @@ def chamfer_rate(dev, iters=20):
     return 16 * 2048 * 2048 / t / 1e9
 
 
+def pair_rate(dev, parts=512, pts=1024):
+    """§8f row 1: all-pairs calc_dcd pseudo-labels over `parts` source parts (upper triangle)."""
+    from engine.generate_pair import PairGenerator, normalize_pts
+    from dataset import synthetic
+    cl = np.stack([normalize_pts(p) for p in synthetic.make_source_db(parts, seed=1)["src_points"][:, :pts]])
+    gen = PairGenerator(torch.from_numpy(cl).to(dev))
+    gen.rows([0])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gen.rows(range(parts))
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    npairs = parts * (parts + 1) // 2
+    return {"parts": parts, "points": pts, "pairs": npairs, "seconds": round(t, 4),
+            "pairs_per_s": round(npairs / t, 1), "gpair_dist_s": round(npairs * pts * pts / t / 1e9, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,6 +258,7 @@ def main():
                                       "tflops": round(v["flop"] / max(v["ms"], 1e-9) / 1e9, 2)}
                                   for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
     extra["chamfer_gpair_s"] = round(chamfer_rate(dev), 1)
+    extra["pseudo_label_dcd"] = pair_rate(dev)
     extra["loss"] = loss_val
     cpu = None if args.no_cpu_baseline else cpu_baseline(args)
     out = {"metric": "train iters/sec chair bs=16 2048-pt @1/2/4/8 GPU; Chamfer Gpair-dist/s",
