@@ -204,27 +204,103 @@ template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; }
 // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
 #define RED(a, q, c) red_f[((a) * 2 + (q)) * BN + (c)]
 #define REDI(a, q, c) red_i[((a) * 2 + (q)) * BN + (c)]
-template <int EPI>
+struct NoPre { __device__ void operator()() const {} };
+
+// Workgroup barrier that orders LDS only. __syncthreads() also carries a release fence for
+// global memory, i.e. a vmcnt(0) that waits for every outstanding store of the wave; the
+// epilogue reductions and the K-loop only exchange data through LDS (the LDS-DMA landing
+// is covered by an explicit vmcnt wait before the barrier).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Output writer. BUF (v2 kernel): every lane issues every store as a buffer store and an
+// out-of-range element gets an offset past num_records (the hardware drops it), so a wave
+// always issues exactly 64 stores per output tile, unconditionally: the persistent kernel
+// relies on that count to wait for its prefetch DMA without waiting for the stores.
+constexpr unsigned ST_OOB = 0x80000000u;
+template <bool BUF>
+struct OutTile {
+    float* base; int ld;
+    unsigned ld4;        // row pitch in bytes, laundered per tile (see below)
+    __amdgpu_buffer_rsrc_t rsrc;
+    __device__ OutTile(float* b, int ld_, int M, int N) : base(b), ld(ld_) {
+        if constexpr (BUF) {
+            rsrc = __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)(((long long)(M - 1) * ld_ + N) * 4), 0x00020000);
+            // opaque to the optimiser: keeps the 64 per-element row products from being
+            // hoisted out of the persistent tile loop (and spilled)
+            ld4 = (unsigned)ld_ * 4u;
+            asm volatile("" : "+s"(ld4));
+        }
+    }
+    __device__ __forceinline__ void put(bool ok, int row, int col, float v) {
+        if constexpr (BUF) {
+            // 32-bit byte offset (buf_ok guarantees M * ld * 4 < 2^31) and a select: no branch
+            const unsigned off = (unsigned)row * ld4 + (unsigned)col * 4u;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc, ok ? off : ST_OOB, 0, 0);
+        } else if (ok) {
+            base[(size_t)row * ld + col] = v;
+        }
+    }
+};
+
+// `pre` runs once all of the epilogue's own global loads are issued and before any of them
+// is consumed: the persistent kernel issues the next tile's first LDS-DMA there, so it lands
+// while this epilogue computes and stores (vmcnt counts in order, so a DMA issued earlier
+// would make every epilogue load wait for it).
+// Matching reader (BN-backward Yp). BUF: buffer loads at 32-bit offsets; rows/columns
+// outside [M, N) read as 0 (their results are never stored). Otherwise clamped loads.
+template <bool BUF>
+struct InTile {
+    const float* base; int ld, M, N;
+    unsigned ld4;
+    __amdgpu_buffer_rsrc_t rsrc;
+    __device__ InTile(const float* b, int ld_, int M_, int N_) : base(b), ld(ld_), M(M_), N(N_) {
+        if constexpr (BUF) {
+            rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), (short)0,
+                                                     (int)(((long long)(M_ - 1) * ld_ + N_) * 4), 0x00020000);
+            ld4 = (unsigned)ld_ * 4u;
+            asm volatile("" : "+s"(ld4));
+        }
+    }
+    __device__ __forceinline__ float get(int row, int col) const {
+        if constexpr (BUF) {
+            const unsigned off = (unsigned)row * ld4 + (unsigned)col * 4u;
+            return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, col < N ? off : ST_OOB, 0, 0));
+        } else {
+            row = row < M ? row : M - 1;
+            col = col < N ? col : N - 1;
+            return base[(size_t)row * ld + col];
+        }
+    }
+};
+
+template <int EPI, bool BUFST = false, class Pre = NoPre>
 __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2], int m0, int n0,
-                                         float* red_f, int* red_i, const f16v* ypre = nullptr) {
+                                         float* red_f, int* red_i, Pre pre = Pre()) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
     // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
     const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
     auto row_of = [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); };
 
     if (EPI == URED_EPI_STORE || EPI == URED_EPI_SPLITK) {
-        float* C = d.C + (EPI == URED_EPI_SPLITK ? (size_t)blockIdx.z * d.M * d.ldc : 0);
+        OutTile<BUFST> C(d.C + (EPI == URED_EPI_SPLITK ? (size_t)blockIdx.z * d.M * d.ldc : 0), d.ldc, d.M, d.N);
+        float bsv[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
-            if (col >= d.N) continue;
-            const float bsv = (EPI == URED_EPI_STORE && d.bias) ? d.bias[col] : 0.f;
+            bsv[j] = (EPI == URED_EPI_STORE && d.bias && col < d.N) ? d.bias[col] : 0.f;
+        }
+        pre();
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = row_of(i, r);
-                    if (row < d.M) C[(size_t)row * d.ldc + col] = acc[i][j][r] + bsv;
+                    C.put(row < d.M && col < d.N, row, col, acc[i][j][r] + bsv[j]);
                 }
         }
         return;
@@ -234,25 +310,36 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
     const int nvalid = min(BM, d.M - m0);
 
     if (EPI == URED_EPI_FWD) {
-        // value, store, per-column block stats (two-pass on registers: mean then M2)
+        // value, store, per-column block stats (two-pass on registers: mean then M2).
+        // Row bias of a block that lies inside one group (group_rows % BM == 0, no gidx):
+        // one load per column, folded into the column bias.
+        const bool rb_blk = d.rowbias && !d.gidx && d.group_rows % BM == 0;
+        OutTile<BUFST> Cw(d.C, d.ldc, d.M, d.N);
+        float bsv_[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
             const bool cv = col < d.N;
-            const float bsv = (cv && d.bias) ? d.bias[col] : 0.f;
+            bsv_[j] = (cv && d.bias) ? d.bias[col] : 0.f;
+            if (rb_blk && cv) bsv_[j] += d.rowbias[(size_t)(m0 / d.group_rows) * d.ldr + col];
+        }
+        pre();
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+            const bool cv = col < d.N;
+            const float bsv = bsv_[j];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = row_of(i, r);
                     float v = acc[i][j][r] + bsv;
-                    if (cv && row < d.M) {
-                        if (d.rowbias) {
-                            const int g = d.gidx ? d.gidx[row] : row / d.group_rows;
-                            v += d.rowbias[(size_t)g * d.ldr + col];
-                        }
-                        d.C[(size_t)row * d.ldc + col] = v;
+                    if (d.rowbias && !rb_blk && cv && row < d.M) {
+                        const int g = d.gidx ? d.gidx[row] : row / d.group_rows;
+                        v += d.rowbias[(size_t)g * d.ldr + col];
                     }
+                    Cw.put(cv && row < d.M, row, col, v);
                     acc[i][j][r] = v;
                 }
         }
@@ -275,7 +362,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
 #pragma unroll
             for (int j = 0; j < 2; ++j) RED(wm, 0, wn * 64 + j * 32 + lane) = csum[j];
         }
-        __syncthreads();
+        lds_barrier();
         float cmean[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -302,7 +389,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
 #pragma unroll
             for (int j = 0; j < 2; ++j) RED(wm, 1, wn * 64 + j * 32 + lane) = cm2[j];
         }
-        __syncthreads();
+        lds_barrier();
         if (wm == 0 && lane < 32) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -315,7 +402,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             }
         }
         if (d.pool_ws) {
-            __syncthreads();
+            lds_barrier();
             // per column max/min of Y with lowest-row tie break
             float mx[2], mn[2];
             int ix[2], in_[2];
@@ -345,7 +432,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                     RED(wm, 1, c) = mn[j]; REDI(wm, 1, c) = in_[j];
                 }
             }
-            __syncthreads();
+            lds_barrier();
             if (wm == 0 && lane < 32) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
@@ -367,47 +454,58 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
 
     if (EPI == URED_EPI_BNBWD) {
         float s1[2], s2[2];
-        // ypre (v2 kernel) holds the j = 0 half of this lane's Yp values, loaded under the last
-        // K-tile; the j = 1 half is issued here so it lands while j = 0 is processed
-        f16v y1[2];
-        if (ypre) {
-            int col = n0 + wn * 64 + 32 + (lane & 31);
-            col = col < d.N ? col : d.N - 1;
+        // Yp one column half (32 values) at a time: the j = 0 half and the per-column
+        // parameters are issued before pre() (the persistent kernel's next-tile DMA), the j = 1
+        // half after the j = 0 half is processed (registers: acc 64 + one half 32)
+        f16v yh[2];
+        InTile<BUFST> Yr(d.Yp, d.ldy, d.M, d.N);
+        auto load_y = [&](int j) {
+            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    int row = row_of(i, r);
-                    row = row < d.M ? row : d.M - 1;
-                    y1[i][r] = d.Yp[(size_t)row * d.ldy + col];
-                }
-        }
+                for (int r = 0; r < 16; ++r) yh[i][r] = Yr.get(row_of(i, r), col);
+        };
+        load_y(0);
         // max-pool backward: the pooled gradient lands on the winning row of each (group, column)
         const bool pool_blk = d.pool_idx && (d.pool_group_rows % BM == 0);
         const int pg = pool_blk ? m0 / d.pool_group_rows : 0;
+        float sc_[2], sh_[2], mu_[2], is_[2], pgr_[2];
+        int pidx_[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
             const bool cv = col < d.N;
             const int cc = cv ? col : 0;
-            const float sc = d.bn_scale[cc], sh = d.bn_shift[cc], mu = d.bn_mean[cc], is = d.bn_invstd[cc];
-            int pidx = -1; float pgr = 0.f;
-            if (pool_blk && cv) { pidx = d.pool_idx[(size_t)pg * d.N + col]; pgr = d.pool_grad[(size_t)pg * d.N + col]; }
+            sc_[j] = d.bn_scale[cc]; sh_[j] = d.bn_shift[cc]; mu_[j] = d.bn_mean[cc]; is_[j] = d.bn_invstd[cc];
+            pidx_[j] = -1; pgr_[j] = 0.f;
+            if (pool_blk && cv) { pidx_[j] = d.pool_idx[(size_t)pg * d.N + col]; pgr_[j] = d.pool_grad[(size_t)pg * d.N + col]; }
+        }
+        pre();
+        OutTile<BUFST> Gw(d.C, d.ldc, d.M, d.N);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (j == 1) load_y(1);
+            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+            const bool cv = col < d.N;
+            const float sc = sc_[j], sh = sh_[j], mu = mu_[j], is = is_[j];
+            const int pidx = pidx_[j];
+            const float pgr = pgr_[j];
             float a1 = 0.f, a2 = 0.f;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = row_of(i, r);
-                    if (!cv || row >= d.M) continue;
+                    const bool ok = cv && row < d.M;
                     float dh = acc[i][j][r];
                     if (pool_blk) {
                         if (row == pidx) dh += pgr;
-                    } else if (d.pool_idx) {
+                    } else if (d.pool_idx && ok) {
                         const size_t ge = (size_t)(row / d.pool_group_rows) * d.N + col;
                         if (d.pool_idx[ge] == row) dh += d.pool_grad[ge];
                     }
-                    const float y = ypre ? (j == 0 ? ypre[i][r] : y1[i][r]) : d.Yp[(size_t)row * d.ldy + col];
+                    const float y = yh[i][r];
                     float g, xh;
                     if (d.bwd_res) {
                         g = dh;
@@ -416,9 +514,9 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                         g = (__builtin_fmaf(y, sc, sh) > 0.f) ? dh : 0.f;
                         xh = (y - mu) * is;
                     }
-                    d.C[(size_t)row * d.ldc + col] = g;
-                    a1 += g;
-                    a2 += g * xh;
+                    Gw.put(ok, row, col, g);
+                    a1 += ok ? g : 0.f;
+                    a2 += ok ? g * xh : 0.f;
                 }
             a1 += __shfl_xor(a1, 32);
             a2 += __shfl_xor(a2, 32);
@@ -431,7 +529,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                 RED(wm, 1, wn * 64 + j * 32 + lane) = s2[j];
             }
         }
-        __syncthreads();
+        lds_barrier();
         if (wm == 0 && lane < 32) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -524,79 +622,64 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
 }
 
 
-// ---- v2: LDS-DMA staged kernel (all-VEC shapes) --------------------------------
-// Both operands reach LDS by global_load_lds_dwordx4 (no VGPR round trip, no staging
+// ---- v2: LDS-DMA staged, persistent kernel (all-VEC shapes) ---------------------
+// Both operands reach LDS by buffer_load_dwordx4 ... lds (no VGPR round trip, no staging
 // registers): a row-major [rows][k] operand lands as a [128][32] image with its 16-B
-// slots XOR-swizzled by (row & 7) (swizzle applied to the per-lane SOURCE address, the
-// LDS image stays lane-linear) and is read 4 consecutive k per ds_read_b128; a k-major
+// slots XOR-swizzled by (row & 7) and is read 4 consecutive k per ds_read_b128; a k-major
 // [k][cols] operand lands as a plain [32][128] image and is read with ds_read_b32.
 // The MFMA k-order is permuted (k-step j of lane half h uses k = 16h + j) so both image
 // kinds feed the same 32x32x2 sequence. The previous layer's BatchNorm+ReLU prologue is
 // applied to the fragments after the LDS read (one fma+max per operand element, hidden
-// under the 64-cycle MFMAs). Two LDS stages, the next tile's DMA in flight during the
-// current tile's MFMAs, one barrier per K-tile.
+// under the 64-cycle MFMAs). Two LDS stages, the next K-step's DMA in flight during the
+// current step's MFMAs, one barrier per K-step; blocks loop over output tiles and the
+// next tile's first step is DMA'd during the current tile's epilogue.
 typedef __attribute__((address_space(3))) void lds_void_t;
-typedef const __attribute__((address_space(1))) void gbl_void_t;
 
-__device__ __forceinline__ void dma16(const float* src, float* lds_base) {
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_base, 16, 0, 0);
-}
-
-// 1024 16-B chunks per 128x32 tile; wave w issues chunks [w*256, w*256+256) as 4 DMAs.
-template <bool KM>
-__device__ __forceinline__ void dma_tile(const float* __restrict__ G, int ld, int ext, int e0, int K, int k0,
-                                         const float* __restrict__ A2, int ld2, int k1, float* S, int w, int lane) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int wi = w * 4 + i;
-        const int c = wi * 64 + lane;
-        const float* src;
-        if constexpr (!KM) {
-            const int r = c >> 3, p = c & 7, sl = p ^ (r & 7);
-            int row = e0 + r;
-            row = row < ext ? row : ext - 1;
-            int k = k0 + 4 * sl;
-            k = k < K ? k : K - 4;
-            src = k < k1 ? G + (size_t)row * ld + k : A2 + (size_t)row * ld2 + (k - k1);
-        } else {
-            const int kk = c >> 5, c4 = c & 31;
-            int k = k0 + kk;
-            k = k < K ? k : K - 1;
-            int col = e0 + 4 * c4;
-            col = col < ext ? col : ext - 4;
-            src = G + (size_t)k * ld + col;
-        }
-        dma16(src, S + wi * 256);
-    }
-}
-
-// Buffer-descriptor form of dma_tile (operands < 2 GiB, no A2 concat): the per-lane byte
-// offsets are computed once per block; a tile only adds its k offset (one VALU add per
-// DMA instead of the clamp/select/64-bit address chain). Lanes whose row (row-major) or
+// 1024 16-B chunks per 128x32 operand image; wave w issues chunks [w*256, w*256+256) as 4
+// buffer-descriptor DMAs (operands < 2 GiB). Row-major: chunk c = (row r = c>>3, slot
+// p = c&7) reads k = 4*(p ^ (r&7)) (the XOR swizzle is on the source address, the LDS image
+// stays lane-linear); k-major: chunk c = (k = c>>5, 4 columns at 4*(c&31)). The per-lane
+// byte offsets are computed once per tile; a K-step only adds its k offset. Lanes whose row (row-major) or
 // column (k-major) is outside the operand get an offset past num_records, and so does any
 // k >= K row of a k-major operand: the hardware returns zeros for them.
 constexpr unsigned BUF_OOB = 0x80000000u;
 constexpr int PRO_LDS = 1024;            // max prologue channels staged in LDS by gemm2
+// Persistent tile loop (next tile's first DMA under the current epilogue). Measured neutral
+// on MI355X once the epilogue stops waiting for its stores (lds_barrier), and it costs
+// SGPR spills (every epilogue argument stays live across the main loop), so it is compiled
+// out; kept for experiments.
+constexpr bool GEMM_PERSIST = false;
 constexpr int BUF_DWORD3 = 0x00020000;   // raw buffer, gfx9 family (gfx950)
 
-__host__ __device__ constexpr bool buf_only_variant(bool b_km, int epi) {
-    return b_km || epi == URED_EPI_BNBWD || epi == URED_EPI_SPLITK;   // A2 concat only feeds forward layers
-}
 __host__ __device__ inline bool buf_ok(const UredGemmDesc& d) {
-    return d.k1 >= d.K &&
+    // a concatenated second A source must start on a K-step boundary (one descriptor per step)
+    const bool a2 = d.k1 >= d.K || (!d.a_kmajor && d.k1 % BK == 0 && d.A2 && (long long)d.M * d.lda2 * 4 < 0x7fffffffLL);
+    return a2 && (long long)d.M * d.ldc * 4 < 0x7fffffffLL && (long long)d.M * d.ldy * 4 < 0x7fffffffLL &&
         (d.a_kmajor ? (long long)d.K * d.lda : (long long)d.M * d.lda) * 4 < 0x7fffffffLL &&
         (d.b_kmajor ? (long long)d.K * d.ldb : (long long)d.N * d.ldb) * 4 < 0x7fffffffLL;
 }
 
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
 struct BufOperand {
-    __amdgpu_buffer_rsrc_t rsrc;
+    i32x4 rsrc;          // raw buffer descriptor: base, stride 0, num_records (bytes), dword3
     unsigned vo[4];
 };
+
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, long long bytes) {
+    const unsigned long long b = reinterpret_cast<unsigned long long>(base);
+    i32x4 r;
+    r.x = (int)(unsigned)(b & 0xffffffffull);
+    r.y = (int)(unsigned)((b >> 32) & 0xffffull);
+    r.z = (int)(unsigned)bytes;
+    r.w = BUF_DWORD3;
+    return r;
+}
 
 template <bool KM>
 __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld, int ext, int e0, int K, int w, int lane) {
     const long long bytes = KM ? ((long long)(K - 1) * ld + ext) * 4 : ((long long)(ext - 1) * ld + K) * 4;
-    o.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)bytes, BUF_DWORD3);
+    o.rsrc = make_rsrc(G, bytes);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int c = (w * 4 + i) * 64 + lane;
@@ -612,12 +695,25 @@ __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld,
     }
 }
 
+// The DMA is issued from inline asm on purpose: the compiler's waitcnt pass then does not
+// track it, so it adds no vmcnt(0) of its own in front of later ds_reads of the stages (it
+// cannot tell the two stages apart, nor count the epilogue's stores behind the prefetch).
+// Completion is ordered explicitly by the K-loop's vmcnt wait before its barrier. Ops the
+// pass cannot see only make its own vmcnt(N) waits conservative (in-order counter). m0 is
+// saved and restored around the instruction.
+__device__ __forceinline__ void dma_lds16(const i32x4& rsrc, unsigned voff, float* lds_dst) {
+    const unsigned lds = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)lds_dst);
+    unsigned saved;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(saved) : "s"(lds), "v"(voff), "s"(rsrc) : "memory");
+}
+
 template <bool KM>
 __device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, float* S, int w) {
     const unsigned toff = KM ? (unsigned)k0 * (unsigned)ld * 4u : (unsigned)k0 * 4u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(o.rsrc, (lds_void_t*)(S + (w * 4 + i) * 256), 16, o.vo[i] + toff, 0, 0, 0);
+    for (int i = 0; i < 4; ++i) dma_lds16(o.rsrc, o.vo[i] + toff, S + (w * 4 + i) * 256);
 }
 
 template <int PRO>
@@ -634,15 +730,15 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     // are staged in LDS once, so a tile reads them with broadcast ds_reads instead of
     // waiting on global (L2) latency every K-step
     constexpr bool PRO_IN_LDS = !A_KM && PRO_A != URED_PRO_NONE;
-    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * TILE + 4 * BN + (PRO_IN_LDS ? 2 * PRO_LDS : 0)];
-    float* red_f = smem + 4 * TILE;                // epilogue scratch (after the stages are drained)
-    float* pro_lds = smem + 4 * TILE + 4 * BN;     // [PRO_LDS] scale, [PRO_LDS] shift
-    int* red_i = reinterpret_cast<int*>(smem);     // pool scratch reuses stage 0 (drained by then)
+    // Separate __shared__ objects: the compiler can then prove the epilogue scratch and the
+    // prologue vectors disjoint from the DMA stages (no vmcnt(0) in front of their ds_reads).
+    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * TILE];
+    __shared__ float red_f[4 * BN];
+    __shared__ int red_i[4 * BN];
+    __shared__ __attribute__((aligned(16))) float pro_lds[PRO_IN_LDS ? 2 * PRO_LDS : 4];   // scale | shift
 
     const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
-    const int tile = xcd_remap(blockIdx.x, ntm * ntn);
-    const int tm_ = tile / ntn, tn_ = tile % ntn;
-    const int m0 = tm_ * BM, n0 = tn_ * BN;
+    const int ntiles = ntm * ntn;
     int kbeg = 0, kend = d.K;
     if (EPI == URED_EPI_SPLITK) {
         const int kps = ((d.K + d.splits - 1) / d.splits + BK - 1) / BK * BK;
@@ -652,64 +748,84 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
     const int h = lane >> 5, li = lane & 31;
 
-    f16v acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    f16v ypre[2];      // BN-backward epilogue operand, j = 0 half (EPI_BNBWD only; dead otherwise)
+    // Persistent over output tiles when the grid is smaller than the tile count (launch()
+    // sizes it to the resident-block slots): tile v -> xcd_remap(v), v += gridDim.x.
+    int v = blockIdx.x;
+    if (v >= ntiles) return;
+    auto tile_origin = [&](int vv, int& m0_, int& n0_) {
+        const int tl = xcd_remap(vv, ntiles);
+        m0_ = (tl / ntn) * BM;
+        n0_ = (tl % ntn) * BN;
+    };
+    int m0, n0;
+    tile_origin(v, m0, n0);
 
-    // k-major B with prologue (wgrad): the channel is this lane's output column, fixed
-    float bs_[2] = {1.f, 1.f}, bt_[2] = {0.f, 0.f};
-    if (PRO_B != URED_PRO_NONE) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            int c = n0 + wn * 64 + j * 32 + li;
-            c = c < d.N ? c : d.N - 1;
-            bs_[j] = d.pro_s[c]; bt_[j] = d.pro_t[c];
-        }
-    }
-
-    // operand bytes < 2 GiB and no concatenated second A source: buffer-descriptor DMA
-    // (variants that never take an A2 are launched only when buf_ok holds, see launch())
-    constexpr bool ONLY_BUF = buf_only_variant(B_KM, EPI);
-    const bool use_buf = ONLY_BUF || buf_ok(d);
-    BufOperand ba, bb;
-    if (use_buf) {
+    // Operands reach LDS by buffer-descriptor DMA (launch() guarantees buf_ok): a
+    // concatenated second A source [M][K-k1] (k1 % BK == 0) gets its own descriptor, chosen
+    // per K-step.
+    const bool has_a2 = !A_KM && d.k1 < d.K;
+    BufOperand ba, ba2, bb;
+    auto setup = [&](int m0_, int n0_) {
         // a k-major operand's rows past kend must read as zero too (split-K: kend < K)
-        buf_setup<A_KM>(ba, d.A, d.lda, d.M, m0, kend, w, lane);
-        buf_setup<B_KM>(bb, d.B, d.ldb, d.N, n0, kend, w, lane);
-    }
-    auto issue = [&](int stage, int k0) {
+        buf_setup<A_KM>(ba, d.A, d.lda, d.M, m0_, A_KM ? kend : min(kend, d.k1), w, lane);
+        if (!A_KM && has_a2) buf_setup<false>(ba2, d.A2, d.lda2, d.M, m0_, d.K - d.k1, w, lane);
+        buf_setup<B_KM>(bb, d.B, d.ldb, d.N, n0_, kend, w, lane);
+    };
+    auto issue = [&](int stage, int k0, int m0_, int n0_) {
         float* As = smem + stage * 2 * TILE;
         float* Bs = As + TILE;
-        if (ONLY_BUF || use_buf) {
-            buf_tile<A_KM>(ba, d.lda, k0, As, w);
-            buf_tile<B_KM>(bb, d.ldb, k0, Bs, w);
-        } else if constexpr (!ONLY_BUF) {
-            dma_tile<A_KM>(d.A, d.lda, d.M, m0, kend, k0, d.A2, d.lda2, d.k1, As, w, lane);
-            dma_tile<B_KM>(d.B, d.ldb, d.N, n0, kend, k0, d.B, 0, 0x7fffffff, Bs, w, lane);
-        }
+        if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false>(ba2, d.lda2, k0 - d.k1, As, w);
+        else buf_tile<A_KM>(ba, d.lda, k0, As, w);
+        buf_tile<B_KM>(bb, d.ldb, k0, Bs, w);
     };
 
     if constexpr (PRO_IN_LDS) {   // visible after the first loop barrier
         for (int i = t; i < d.k1; i += NT) { pro_lds[i] = d.pro_s[i]; pro_lds[PRO_LDS + i] = d.pro_t[i]; }
     }
-    if (kbeg < kend) {
-        issue(0, kbeg);
-        int stage = 0;
+    const bool has_k = kbeg < kend;
+    bool after_epi = false;
+    int stage = 0;
+    setup(m0, n0);
+    if (has_k) issue(0, kbeg, m0, n0);
+
+    while (true) {
+        f16v acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+        // k-major B with prologue (wgrad): the channel is this lane's output column, fixed
+        float bs_[2] = {1.f, 1.f}, bt_[2] = {0.f, 0.f};
+        if (PRO_B != URED_PRO_NONE) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                int c = n0 + wn * 64 + j * 32 + li;
+                c = c < d.N ? c : d.N - 1;
+                bs_[j] = d.pro_s[c]; bt_[j] = d.pro_t[c];
+            }
+            // Re-define the loaded values through an asm so the compiler's wait for these loads
+            // sits here, once, and not inside the K-loop, where the hardware counter also holds
+            // the (compiler-invisible) next-step DMA and a vmcnt(0) would expose it every step.
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(bs_[0]), "+v"(bs_[1]), "+v"(bt_[0]), "+v"(bt_[1]));
+        }
+
         for (int k0 = kbeg; k0 < kend; k0 += BK) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
+            // This wave's share of the step's DMA must have landed before the barrier. After an
+            // epilogue, the 64 output stores it issued after the prefetch DMA (OutTile) may still
+            // be draining: vmcnt counts in order on gfx9, so <= 63 outstanding covers the DMA.
+            if (k0 == kbeg && after_epi) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_barrier();
             const float* As = smem + stage * 2 * TILE;
             const float* Bs = As + TILE;
             const bool tail = k0 + BK > kend;
 
-            // ---- every fragment of this tile goes LDS -> VGPR before the next tile's DMA is
-            // issued: the compiler orders a global_load_lds before any later ds_read with a
-            // vmcnt(0) (it cannot prove the stages disjoint), which would expose the prefetch.
+            // ---- every fragment of this K-step goes LDS -> VGPR before the next step's DMA
+            // is issued: the compiler orders a global_load_lds before any later ds_read of the
+            // same __shared__ object with a vmcnt(0), which would expose the prefetch.
             // a[tm][j], b[tn][j] for k = k0 + 16h + j
             float a[2][16], b[2][16];
             if constexpr (!A_KM) {
@@ -718,8 +834,8 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                     const int r = wm * 64 + tm * 32 + li;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const float4 v = *reinterpret_cast<const float4*>(As + r * 32 + 4 * ((4 * h + q) ^ (r & 7)));
-                        a[tm][4 * q] = v.x; a[tm][4 * q + 1] = v.y; a[tm][4 * q + 2] = v.z; a[tm][4 * q + 3] = v.w;
+                        const float4 v4 = *reinterpret_cast<const float4*>(As + r * 32 + 4 * ((4 * h + q) ^ (r & 7)));
+                        a[tm][4 * q] = v4.x; a[tm][4 * q + 1] = v4.y; a[tm][4 * q + 2] = v4.z; a[tm][4 * q + 3] = v4.w;
                     }
                 }
             } else {
@@ -734,16 +850,14 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                 if constexpr (!B_KM) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const float4 v = *reinterpret_cast<const float4*>(Bs + cidx * 32 + 4 * ((4 * h + q) ^ (cidx & 7)));
-                        b[tn][4 * q] = v.x; b[tn][4 * q + 1] = v.y; b[tn][4 * q + 2] = v.z; b[tn][4 * q + 3] = v.w;
+                        const float4 v4 = *reinterpret_cast<const float4*>(Bs + cidx * 32 + 4 * ((4 * h + q) ^ (cidx & 7)));
+                        b[tn][4 * q] = v4.x; b[tn][4 * q + 1] = v4.y; b[tn][4 * q + 2] = v4.z; b[tn][4 * q + 3] = v4.w;
                     }
                 } else {
 #pragma unroll
                     for (int j = 0; j < 16; ++j) b[tn][j] = Bs[(16 * h + j) * BN + cidx];
                 }
             }
-            // the prologue's per-channel scale/shift: global loads issued BEFORE the DMA, so
-            // waiting for them (vmcnt counts in order) does not wait for the next tile
             float ss[16], tt[16];
             bool raw = false;
             if constexpr (PRO_IN_LDS) {
@@ -758,21 +872,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                     tt[4 * q] = tv.x; tt[4 * q + 1] = tv.y; tt[4 * q + 2] = tv.z; tt[4 * q + 3] = tv.w;
                 }
             }
-            if (k0 + BK < kend) {
-                issue(stage ^ 1, k0 + BK);   // lands while this tile is multiplied
-            } else if constexpr (EPI == URED_EPI_BNBWD) {
-                // last tile: the BN-backward epilogue's Yp tile streams in under its MFMAs
-                int col = n0 + wn * 64 + li;
-                col = col < d.N ? col : d.N - 1;
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        int row = m0 + wm * 64 + 4 * h + i * 32 + (r & 3) + 8 * (r >> 2);
-                        row = row < d.M ? row : d.M - 1;
-                        ypre[i][r] = d.Yp[(size_t)row * d.ldy + col];
-                    }
-            }
+            if (k0 + BK < kend) issue(stage ^ 1, k0 + BK, m0, n0);   // lands while this step is multiplied
 
             // ---- prologues (previous layer's BN+ReLU) and the K tail, on the fragments
             if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
@@ -806,9 +906,23 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             }
             stage ^= 1;
         }
-        __syncthreads();   // all waves done with the stages before the epilogue reuses LDS
+
+        // The stage `stage` was last read one K-step ago (a barrier has passed since), so the
+        // next tile's first step can be DMA'd into it while this tile's epilogue runs.
+        const int nv = v + gridDim.x;
+        int nm0 = 0, nn0 = 0;
+        if (GEMM_PERSIST && nv < ntiles) tile_origin(nv, nm0, nn0);
+        auto pre = [&]() {
+            if (GEMM_PERSIST && nv < ntiles) {
+                setup(nm0, nn0);
+                if (has_k) issue(stage, kbeg, nm0, nn0);
+            }
+        };
+        epilogue<EPI, true>(d, acc, m0, n0, red_f, red_i, pre);
+        if (!GEMM_PERSIST || nv >= ntiles) break;
+        v = nv; m0 = nm0; n0 = nn0;
+        after_epi = true;
     }
-    epilogue<EPI>(d, acc, m0, n0, red_f, red_i, EPI == URED_EPI_BNBWD && kbeg < kend ? ypre : nullptr);
 }
 
 // ---- small kernels -------------------------------------------------------------
@@ -1052,12 +1166,33 @@ bool v2_ok(const UredGemmDesc& d) {
     return true;
 }
 
+// Resident-block slots of the current device for the persistent v2 kernel (2 blocks of 256
+// threads per CU: VGPR-bound), a multiple of 8 so that blockIdx % 8 stays the XCD.
+// URED_GEMM_PERSIST=0 launches one block per tile instead.
+int persist_slots() {
+    static const bool on = [] { const char* e = getenv("URED_GEMM_PERSIST"); return !(e && e[0] == '0'); }();
+    if (!on) return 0;
+    thread_local int dev_cached = -1, slots = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (dev != dev_cached) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+        slots = (2 * cus) / 8 * 8;
+        dev_cached = dev;
+    }
+    return slots;
+}
+
 template <bool A_KM, bool B_KM, int PA, int PB, int EPI>
 void launch(const UredGemmDesc& d, hipStream_t st) {
     const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
     dim3 grid(ntm * ntn, 1, EPI == URED_EPI_SPLITK ? d.splits : 1);
-    if (vec_ok(d) && v2_ok(d) && (!buf_only_variant(B_KM, EPI) || buf_ok(d)))
+    if (vec_ok(d) && v2_ok(d) && buf_ok(d)) {
+        const int slots = (EPI == URED_EPI_SPLITK || !GEMM_PERSIST) ? 0 : persist_slots();
+        if (slots > 0 && (int)grid.x > slots) grid.x = slots;
         hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI>), grid, dim3(NT), 0, st, d);
+    }
     else if (vec_ok(d)) hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, true>), grid, dim3(NT), 0, st, d);
     else hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, false>), grid, dim3(NT), 0, st, d);
 }
