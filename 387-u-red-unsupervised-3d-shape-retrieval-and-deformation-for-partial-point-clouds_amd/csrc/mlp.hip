@@ -927,15 +927,32 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
 
 // ---- small kernels -------------------------------------------------------------
 
-__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
-                                     float* __restrict__ out, int ldo, int accumulate) {
+// out[m][n] (+)= sum_z ws[z][m][n]. Block = 64 consecutive elements x 4 waves; wave w sums
+// splits w, w+4, ... with four independent accumulators; fixed combine order (deterministic).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                            float* __restrict__ out, int ldo, int accumulate) {
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const size_t total = (size_t)M * N;
-    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
-        const int m = e / N, n = e % N;
-        float s = 0.f;
-        for (int z = 0; z < splits; ++z) s += ws[(size_t)z * total + e];
+    const size_t e = (size_t)blockIdx.x * 64 + lane;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (e < total) {
+        int z = w;
+        for (; z + 12 < splits; z += 16) {
+            a0 += ws[(size_t)z * total + e];
+            a1 += ws[(size_t)(z + 4) * total + e];
+            a2 += ws[(size_t)(z + 8) * total + e];
+            a3 += ws[(size_t)(z + 12) * total + e];
+        }
+        for (; z < splits; z += 4) a0 += ws[(size_t)z * total + e];
+    }
+    part[w][lane] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (w == 0 && e < total) {
+        const float sum = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+        const int m = (int)(e / N), n = (int)(e % N);
         float* o = out + (size_t)m * ldo + n;
-        *o = accumulate ? *o + s : s;
+        *o = accumulate ? *o + sum : sum;
     }
 }
 
@@ -1123,22 +1140,39 @@ __global__ __launch_bounds__(256) void pool_rows_kernel(const float* __restrict_
 }
 
 // out[g][n] = sum of rows [r0, r1) of column n. Block = 4 waves x 64 columns; wave w sums
-// rows r0+w, r0+w+4, ... (a wave reads 256 contiguous bytes per row), waves combined in LDS
-// in fixed order: deterministic.
+// rows r0+w, r0+w+4, ... with four independent accumulators (16 rows in flight per lane; a
+// wave reads 256 contiguous bytes per row), combined in a fixed order and across waves in
+// LDS: deterministic. blockIdx.z = split s of S: the group's rows are cut into S equal
+// ranges and split s writes ws[g][s][n] (S > 1) for a second pass over the S partials.
 __global__ __launch_bounds__(256) void group_colsum_kernel(const float* __restrict__ X, int ldx, int N,
         const int* __restrict__ off, int group_rows, float* __restrict__ out, int ldo) {
     __shared__ float part[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int n = blockIdx.x * 64 + lane;
-    const int g = blockIdx.y;
-    const int r0 = off ? off[g] : g * group_rows;
-    const int r1 = off ? off[g + 1] : (g + 1) * group_rows;
-    float s = 0.f;
-    if (n < N)
-        for (int r = r0 + w; r < r1; r += 4) s += X[(size_t)r * ldx + n];
-    part[w][lane] = s;
+    const int g = blockIdx.y, S = gridDim.z, sp = blockIdx.z;
+    const int g0 = off ? off[g] : g * group_rows;
+    const int g1 = off ? off[g + 1] : (g + 1) * group_rows;
+    const long long len = g1 - g0;
+    const int r0 = g0 + (int)(len * sp / S), r1 = g0 + (int)(len * (sp + 1) / S);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (n < N) {
+        const float* col = X + n;
+        int r = r0 + w;
+        for (; r + 12 < r1; r += 16) {
+            a0 += col[(size_t)r * ldx];
+            a1 += col[(size_t)(r + 4) * ldx];
+            a2 += col[(size_t)(r + 8) * ldx];
+            a3 += col[(size_t)(r + 12) * ldx];
+        }
+        for (; r < r1; r += 4) a0 += col[(size_t)r * ldx];
+    }
+    part[w][lane] = (a0 + a1) + (a2 + a3);
     __syncthreads();
-    if (w == 0 && n < N) out[(size_t)g * ldo + n] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    if (w == 0 && n < N) {
+        const float v = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+        if (S == 1) out[(size_t)g * ldo + n] = v;
+        else out[((size_t)g * S + sp) * N + n] = v;
+    }
 }
 
 // VEC (float4 staging) needs 16-B aligned rows and contiguous extents that are multiples of 4.
@@ -1267,8 +1301,9 @@ int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, in
     if (M == 0 || N == 0) return 0;
     URED_REQUIRE(ws && out, "ured_splitk_reduce: null pointer");
     const size_t total = (size_t)M * N;
-    const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ws, splits, M, N, out, ldo, accumulate);
+    URED_REQUIRE((total + 63) / 64 <= 0x7fffffff, "ured_splitk_reduce: too many elements");
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
+                       ws, splits, M, N, out, ldo, accumulate);
     return ured::launch_status("ured_splitk_reduce");
 }
 
@@ -1342,13 +1377,26 @@ int ured_pool_rows(const float* Y, int M, int N, int group_rows, const float* sc
 
 int ured_group_colsum(const float* X, int ldx, int N, const int* off, int group_rows, int G,
                       float* out, int ldo, void* stream) {
+    return ured_group_colsum_split(X, ldx, N, off, group_rows, G, 1, nullptr, out, ldo, stream);
+}
+
+int ured_group_colsum_split(const float* X, int ldx, int N, const int* off, int group_rows, int G, int splits,
+                            float* ws, float* out, int ldo, void* stream) {
     ured::clear_error();
     URED_REQUIRE(N >= 0 && G >= 0 && ldx >= N && ldo >= N, "ured_group_colsum: bad sizes");
+    URED_REQUIRE(splits >= 1 && splits <= 1024, "ured_group_colsum: splits=%d outside [1, 1024]", splits);
     if (N == 0 || G == 0) return 0;
     URED_REQUIRE(X && out && (off || group_rows > 0), "ured_group_colsum: null pointer / no grouping");
+    URED_REQUIRE(splits == 1 || ws, "ured_group_colsum: splits > 1 needs a workspace [G][splits][N]");
     URED_REQUIRE(G <= 65535, "ured_group_colsum: G=%d > 65535", G);
-    dim3 grid((N + 63) / 64, G);
-    hipLaunchKernelGGL(group_colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, ldx, N, off, group_rows, out, ldo);
+    dim3 grid((N + 63) / 64, G, splits);
+    hipLaunchKernelGGL(group_colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, ldx, N, off, group_rows,
+                       splits == 1 ? out : ws, ldo);
+    if (splits > 1) {   // second pass: the S partials of each group, in split order
+        dim3 grid2((N + 63) / 64, G, 1);
+        hipLaunchKernelGGL(group_colsum_kernel, grid2, dim3(256), 0, (hipStream_t)stream, ws, N, N, nullptr, splits,
+                           out, ldo);
+    }
     return ured::launch_status("ured_group_colsum");
 }
 

@@ -36,6 +36,7 @@ _SIGS = {
     "ured_bn_bwd_apply": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "ured_pool_finalize": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_group_colsum": [_P, _I, _I, _P, _I, _I, _P, _I, _P],
+    "ured_group_colsum_split": [_P, _I, _I, _P, _I, _I, _I, _P, _P, _I, _P],
     "ured_pool_rows": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
 }
 _lib.register(_SIGS)
@@ -140,36 +141,27 @@ def pool_rows(Y, group_rows, scale, shift):
     return pooled, argidx
 
 
-def group_colsum(X, N, G, *, off=None, group_rows=0, ldx=None, out=None):
+def group_colsum(X, N, G, *, off=None, group_rows=0, ldx=None, out=None, rows=None):
+    """out[g] = column sums of rows [off[g], off[g+1]) (or fixed group_rows) of X[:, :N].
+    Long groups are split over more workgroups (ured_group_colsum_split); `rows` = total
+    rows covered (defaults to G * group_rows, or X.shape[0] for ragged groups)."""
     out = torch.empty(G, N, device=X.device) if out is None else out
-    _lib.call("ured_group_colsum", _p(X), int(N if ldx is None else ldx), int(N), _p(off), int(group_rows), int(G),
-              _p(out), int(out.stride(0)), _lib.stream_of(X))
+    rows = (G * group_rows if off is None else X.shape[0]) if rows is None else rows
+    per = max(1, rows // max(G, 1))
+    blocks = ((N + 63) // 64) * G
+    splits = 1
+    while per // (splits * 2) >= 256 and blocks * splits < 2048 and splits < 256:
+        splits *= 2
+    ws = torch.empty(G, splits, N, device=X.device) if splits > 1 else None
+    _lib.call("ured_group_colsum_split", _p(X), int(N if ldx is None else ldx), int(N), _p(off), int(group_rows),
+              int(G), int(splits), _p(ws), _p(out), int(out.stride(0)), _lib.stream_of(X))
     return out
 
 
-_OFF_CACHE = {}
-
-
-def _chunk_offsets(R, chunk, device):
-    key = (R, chunk, str(device))
-    off = _OFF_CACHE.get(key)
-    if off is None:
-        nch = (R + chunk - 1) // chunk
-        o = [min(i * chunk, R) for i in range(nch + 1)]
-        off = torch.tensor(o, dtype=torch.int32, device=device)
-        _OFF_CACHE[key] = off
-    return off
-
-
 def colsum(X):
-    """Column sums of a [R][N] tensor: deterministic two-level reduction (chunks of 64 rows)."""
+    """Column sums of a [R][N] tensor (deterministic: fixed split ranges and combine order)."""
     R, N = X.shape
-    if R <= 256:
-        return group_colsum(X, N, 1, group_rows=R)[0]
-    chunk = 64
-    off = _chunk_offsets(R, chunk, X.device)
-    part = group_colsum(X, N, off.shape[0] - 1, off=off)
-    return colsum(part)
+    return group_colsum(X, N, 1, group_rows=R)[0]
 
 
 def splitk_reduce(ws, splits, M, N, out, ldo, accumulate=False, out_off=0):

@@ -164,7 +164,7 @@ class PointEncoderFn(Function):
                 if i == 5:   # semantic columns of fuse_sem
                     S = sem.shape[1]
                     if spec.mode == "src":
-                        D = K.group_colsum(dYi, N, G, group_rows=GR)
+                        D = _group_sums(dYi, cs, N, G, GR)
                         K.wgrad(D, N, sem, S, N, S, G, dW, W.shape[1], out_off=kin)
                     else:
                         K.wgrad(dYi, N, sem, S, N, S, M, dW, W.shape[1], out_off=kin)
@@ -173,6 +173,15 @@ class PointEncoderFn(Function):
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
         return (None, None, None) + tuple(grads)
+
+
+def _group_sums(dY, cs, N, G, group_rows):
+    """Per-group column sums of dY [G*group_rows, N]. When groups are whole 128-row blocks they
+    come from the BN-backward apply's per-block partials cs [M/128, N] (8 MB instead of
+    re-reading the 1 GB gradient)."""
+    if group_rows % K.BM == 0:
+        return K.group_colsum(cs, N, G, group_rows=group_rows // K.BM)
+    return K.group_colsum(dY, N, G, group_rows=group_rows)
 
 
 class ResidualNetFn(Function):
@@ -278,7 +287,7 @@ class ResidualNetFn(Function):
                     if off is not None:
                         D = K.group_colsum(dYi, N, G, off=off)
                     else:
-                        D = K.group_colsum(dYi, N, G, group_rows=group_rows)
+                        D = _group_sums(dYi, cs, N, G, group_rows)
                     K.wgrad(D, N, code, Cc, N, Cc, G, dW, ld1, out_off=code_off)
             else:
                 Xp, stp = Ys[i - 1], states[i - 1]

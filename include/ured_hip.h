@@ -184,6 +184,11 @@ int ured_pool_rows(const float* Y, int M, int N, int group_rows, const float* sc
  * fixed groups of group_rows rows. G groups. */
 int ured_group_colsum(const float* X, int ldx, int N, const int* off, int group_rows, int G,
                       float* out, int ldo, void* stream);
+/* As ured_group_colsum, with each group's rows cut into `splits` equal ranges summed by
+ * separate workgroups into ws [G][splits][N], then the partials summed in split order
+ * (deterministic; for few, long groups). splits == 1: ws may be NULL. */
+int ured_group_colsum_split(const float* X, int ldx, int N, const int* off, int group_rows, int G, int splits,
+                            float* ws, float* out, int ldo, void* stream);
 
 #ifdef __cplusplus
 }
