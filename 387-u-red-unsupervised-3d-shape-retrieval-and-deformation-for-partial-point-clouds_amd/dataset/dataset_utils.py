@@ -32,7 +32,10 @@ def get_shape(A, param, src_default_param=None, weight=1.0, param_init=None, con
 
 
 def get_symmetric(pc):
-    return pc * pc.new_tensor([-1.0, 1.0, 1.0])
+    """x -> -x reflection (dataset_utils.py:1194-1196). Built without a host-made constant
+    tensor (an H2D copy is not allowed inside HIP-graph capture); negation is exact, so the
+    values equal the reference's multiply by [-1, 1, 1]."""
+    return torch.cat((-pc[..., :1], pc[..., 1:]), dim=-1)
 
 
 def _index(source_labels, db):

@@ -52,5 +52,5 @@ def compute_contrast_loss_loss(tgt_part_f, src_f, src_labels, differentiable_gat
     t_e = F.normalize(t, dim=-1, p=2)
     s_e = F.normalize(s, dim=-1, p=2)
     _, s_all = all_gather_batch([t_e, s_e], differentiable=differentiable_gather)
-    scale = torch.tensor(LOGIT_SCALE, device=t.device).exp()
+    scale = torch.full((), LOGIT_SCALE, device=t.device).exp()   # a fill kernel: graph-capturable (no H2D copy)
     return F.cross_entropy(scale * t_e @ s_all.t(), labels, ignore_index=-1)

@@ -16,6 +16,8 @@ def define_optimizer_dm_re_recon(target_encoder_full, param_decoder_full, recon_
         kw = {}
         if params and params[0].is_cuda and cfg.get("fused_adam", True):
             kw["fused"] = True
+        if params and params[0].is_cuda and cfg.get("cuda_graph", False):
+            kw["capturable"] = True   # step counters on device: the step can be replayed as a HIP graph
         opt = torch.optim.Adam(params, lr=cfg["learning_rate"], betas=(0.9, 0.999), eps=1e-8,
                                weight_decay=cfg["weight_decay"], **kw)
     else:

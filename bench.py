@@ -170,6 +170,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true")
     ap.add_argument("--shapes-out", default=None, help="write the per-shape GEMM breakdown (JSON) here")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as HIP graphs (engine/graph.py; N=1 unless --graph-dp). Measured "
+                         "equal to eager once the step has no host syncs, so eager is the default")
+    ap.add_argument("--graph-dp", action="store_true", help="HIP-graph replay also when N > 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,10 +192,17 @@ def main():
     from dataset import synthetic
 
     cfg = workload_cfg(args)
+    use_graph = args.graph and (world == 1 or args.graph_dp)
+    cfg["cuda_graph"] = use_graph
     db, _ = load_sources(cfg, dev)
-    step = DataParallelStep(cfg, db, dev)
+    eager = DataParallelStep(cfg, db, dev)
     batches = [batch_to_device(synthetic.make_batch(args.batch, args.points, db.num_sources, parts=args.parts,
                                                     seed=1000 * rank + i), dev) for i in range(4)]
+    if use_graph:   # capture (after 3 eager warm-up steps on batch 0); replays below
+        from engine.graph import GraphedStep
+        step = GraphedStep(eager, batches[0])
+    else:
+        step = eager
 
     for i in range(args.warmup):
         step.step(batches[i % 4])
@@ -215,8 +226,8 @@ def main():
 
     breakdown = None
     if not args.no_breakdown:
-        with GemmTimer() as gt:
-            step.step(batches[0])
+        with GemmTimer() as gt:   # one eager step (same kernels) with per-launch events
+            eager.step(batches[0])
         breakdown = gt.summary()
         if args.shapes_out and rank == 0:
             with open(args.shapes_out, "w") as f:
@@ -264,6 +275,7 @@ def main():
     out = {"metric": "train iters/sec chair bs=16 2048-pt @1/2/4/8 GPU; Chamfer Gpair-dist/s",
            "value": round(iters_per_s * world, 4), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+           "step_mode": "hip_graph" if use_graph else "eager",
            "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY §8d generator; random-init weights)",
            "config": {"workload": "config 2: chair, full U-RED train step, bs=16/GPU, 2048 pts, 16x1024 source pts, "
                                   "C=512, S=128, 4 parts/target", "global_batch": args.batch * world,

@@ -1,0 +1,46 @@
+"""torch.profiler view of one config-2 train step: which torch ops launch the small kernels.
+
+  python tools/torch_prof.py [--steps 2] > out.txt
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+ge.add_pkg_path()
+import torch  # noqa: E402
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=2)
+    a = ap.parse_args()
+    import bench
+    from engine.dp import DataParallelStep
+    from engine.train import batch_to_device
+    from train_utils.load_sources import load_sources
+    from dataset import synthetic
+
+    class Args:
+        batch, points, parts, sources = 16, 2048, 4, 512
+    cfg = bench.workload_cfg(Args)
+    dev = torch.device("cuda:0")
+    db, _ = load_sources(cfg, dev)
+    step = DataParallelStep(cfg, db, dev)
+    batches = [batch_to_device(synthetic.make_batch(16, 2048, db.num_sources, parts=4, seed=i), dev) for i in range(2)]
+    for i in range(3):
+        step.step(batches[i % 2])
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=False) as prof:
+        for i in range(a.steps):
+            step.step(batches[i % 2])
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by="self_device_time_total", row_limit=70, max_name_column_width=60))
+    print(prof.key_averages(group_by_stack_n=0).table(sort_by="count", row_limit=40, max_name_column_width=60))
+
+
+if __name__ == "__main__":
+    main()
