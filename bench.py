@@ -79,7 +79,7 @@ class GemmTimer:
             d["bytes"] += 4.0 * (M * K + K * N + M * N) + extra
         return by
 
-    def shapes(self):
+    def shapes(self, steps=1):
         torch.cuda.synchronize()
         by = {}
         for epi, ak, bk, pa, pb, M, N, K, e0, e1 in self.rec:
@@ -88,6 +88,9 @@ class GemmTimer:
             d["launches"] += 1
             d["ms"] += e0.elapsed_time(e1)
             d["tflops"] = round(2.0 * M * N * K * d["launches"] / (d["ms"] * 1e-3) / 1e12, 1)
+        for d in by.values():   # per step
+            d["launches"] /= steps
+            d["ms"] /= steps
         return dict(sorted(by.items(), key=lambda kv: -kv[1]["ms"]))
 
 
@@ -169,6 +172,7 @@ def main():
     ap.add_argument("--sources", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true")
+    ap.add_argument("--breakdown-steps", type=int, default=3, help="eager steps timed per GEMM launch after the run")
     ap.add_argument("--shapes-out", default=None, help="write the per-shape GEMM breakdown (JSON) here")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as HIP graphs (engine/graph.py; N=1 unless --graph-dp). Measured "
@@ -226,12 +230,16 @@ def main():
 
     breakdown = None
     if not args.no_breakdown:
-        with GemmTimer() as gt:   # one eager step (same kernels) with per-launch events
-            eager.step(batches[0])
+        with GemmTimer() as gt:   # eager steps (same kernels) with per-launch events
+            for i in range(args.breakdown_steps):
+                eager.step(batches[i % 4])
         breakdown = gt.summary()
+        for v in breakdown.values():   # per-step figures
+            for k in ("launches", "ms", "flop", "bytes"):
+                v[k] /= args.breakdown_steps
         if args.shapes_out and rank == 0:
             with open(args.shapes_out, "w") as f:
-                json.dump(gt.shapes(), f, indent=1)
+                json.dump(gt.shapes(args.breakdown_steps), f, indent=1)
 
     if rank != 0:
         if world > 1:
@@ -259,13 +267,13 @@ def main():
                     "frac": round(ach / PEAK_FP32_TFLOPS, 4),
                     "traffic": None if traffic is None else round(traffic), "traffic_source": tsrc,
                     "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
-                    "kernel": dom_key, "launches_per_step": d["launches"], "avg_launch_ms": round(avg_ms, 4),
+                    "kernel": dom_key, "launches_per_step": round(d["launches"], 2), "avg_launch_ms": round(avg_ms, 4),
                     "flop_per_launch": round(flop_per_launch)}
         tot_ms = sum(v["ms"] for v in breakdown.values())
         tot_flop = sum(v["flop"] for v in breakdown.values())
         extra["gemm_all"] = {"ms_per_step": round(tot_ms, 3), "tflop_per_step": round(tot_flop / 1e12, 4),
                              "tflops": round(tot_flop / (tot_ms * 1e-3) / 1e12, 2)}
-        extra["gemm_variants"] = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+        extra["gemm_variants"] = {k: {"launches": round(v["launches"], 2), "ms": round(v["ms"], 3),
                                       "tflops": round(v["flop"] / max(v["ms"], 1e-9) / 1e9, 2)}
                                   for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
     extra["chamfer_gpair_s"] = round(chamfer_rate(dev), 1)
