@@ -33,6 +33,7 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
 
 typedef float f16v __attribute__((ext_vector_type(16)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 struct Gemm {
     UredGemmDesc d;
@@ -822,11 +823,28 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             const float* As = smem + stage * 2 * TILE;
             const float* Bs = As + TILE;
             const bool tail = k0 + BK > kend;
+            // next step's DMA first (into the other stage: its last readers passed the barrier
+            // above); it lands while this step is read and multiplied
+            if (k0 + BK < kend) issue(stage ^ 1, k0 + BK, m0, n0);
 
-            // ---- every fragment of this K-step goes LDS -> VGPR before the next step's DMA
-            // is issued: the compiler orders a global_load_lds before any later ds_read of the
-            // same __shared__ object with a vmcnt(0), which would expose the prefetch.
-            // a[tm][j], b[tn][j] for k = k0 + 16h + j
+            // the prologue's scale/shift first: LDS reads complete in issue order, so the
+            // prologue (and the MFMAs behind it) can start on the first A fragments
+            float ss[16], tt[16];
+            // k1 (start of the raw concatenated A2) is a multiple of BK when A2 is present
+            // (buf_ok), so "this K-step needs the prologue" is wave-uniform: a scalar branch
+            // instead of a per-element select
+            const bool pro_step = PRO_IN_LDS && k0 < d.k1;
+            if (pro_step) {
+                const int kc = min(k0 + 16 * h, d.k1 - 16);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 sv = *reinterpret_cast<const float4*>(pro_lds + kc + 4 * q);
+                    const float4 tv = *reinterpret_cast<const float4*>(pro_lds + PRO_LDS + kc + 4 * q);
+                    ss[4 * q] = sv.x; ss[4 * q + 1] = sv.y; ss[4 * q + 2] = sv.z; ss[4 * q + 3] = sv.w;
+                    tt[4 * q] = tv.x; tt[4 * q + 1] = tv.y; tt[4 * q + 2] = tv.z; tt[4 * q + 3] = tv.w;
+                }
+            }
+            // ---- fragments LDS -> VGPR: a[tm][j], b[tn][j] for k = k0 + 16h + j
             float a[2][16], b[2][16];
             if constexpr (!A_KM) {
 #pragma unroll
@@ -858,31 +876,21 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                     for (int j = 0; j < 16; ++j) b[tn][j] = Bs[(16 * h + j) * BN + cidx];
                 }
             }
-            float ss[16], tt[16];
-            bool raw = false;
-            if constexpr (PRO_IN_LDS) {
-                int kc = k0 + 16 * h;
-                raw = kc >= d.k1;
-                kc = raw ? d.k1 - 16 : kc;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 sv = *reinterpret_cast<const float4*>(pro_lds + kc + 4 * q);
-                    const float4 tv = *reinterpret_cast<const float4*>(pro_lds + PRO_LDS + kc + 4 * q);
-                    ss[4 * q] = sv.x; ss[4 * q + 1] = sv.y; ss[4 * q + 2] = sv.z; ss[4 * q + 3] = sv.w;
-                    tt[4 * q] = tv.x; tt[4 * q + 1] = tv.y; tt[4 * q + 2] = tv.z; tt[4 * q + 3] = tv.w;
-                }
-            }
-            if (k0 + BK < kend) issue(stage ^ 1, k0 + BK, m0, n0);   // lands while this step is multiplied
 
             // ---- prologues (previous layer's BN+ReLU) and the K tail, on the fragments
             if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
+                if (pro_step) {
+                    // the two M-halves share channel j: one packed fma (v_pk_fma_f32) per pair
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-#pragma unroll
-                        for (int tm = 0; tm < 2; ++tm)
-                            a[tm][4 * q + e] = raw ? a[tm][4 * q + e] : pro_v<PRO_A>(a[tm][4 * q + e], ss[4 * q + e], tt[4 * q + e]);
+                    for (int j = 0; j < 16; ++j) {
+                        f2v v = {a[0][j], a[1][j]};
+                        const f2v sv = {ss[j], ss[j]}, tv = {tt[j], tt[j]};
+                        if (PRO_A == URED_PRO_RES) v = (f2v){fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+                        v = __builtin_elementwise_fma(v, sv, tv);
+                        if (PRO_A == URED_PRO_ENC) v = (f2v){fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+                        a[0][j] = v.x; a[1][j] = v.y;
+                    }
+                }
             }
             if constexpr (B_KM && PRO_B != URED_PRO_NONE) {
 #pragma unroll
