@@ -965,34 +965,47 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 // one block (256 threads) per column; fp64 fixed-order tree reductions
+// Row multiplicities (unique-row training, see DESIGN "unique source encoding"): when gw is
+// non-null, every row of group g = row / grows stands for gw[g] identical rows of the full
+// batch. grows is a multiple of BM, so a partial block has one weight: its count scales by w,
+// its M2 by w, its mean is unchanged (Chan merge with weighted counts).
+__device__ __forceinline__ double blk_weight(const float* gw, int grows, int b) {
+    return gw ? (double)gw[(b * BM) / grows] : 1.0;
+}
+
 __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ ws, int M, int N,
         const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
-        float* running_mean, float* running_var, float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
-    __shared__ double sh[256];
+        float* running_mean, float* running_var, float* mean_o, float* invstd_o, float* scale_o, float* shift_o,
+        const float* __restrict__ gw, int grows) {
+    __shared__ double sh[256], shc[256];
     const int n = blockIdx.x, t = threadIdx.x;
     const int nblk = (M + BM - 1) / BM;
-    double s = 0.0;
+    double s = 0.0, c = 0.0;
     for (int b = t; b < nblk; b += 256) {
-        const int cnt = min(BM, M - b * BM);
-        s += (double)cnt * (double)ws[(size_t)b * 2 * N + n];
+        const double cnt = (double)min(BM, M - b * BM) * blk_weight(gw, grows, b);
+        s += cnt * (double)ws[(size_t)b * 2 * N + n];
+        c += cnt;
     }
     sh[t] = s;
+    shc[t] = c;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) { if (t < o) sh[t] += sh[t + o]; __syncthreads(); }
-    const double mean = sh[0] / (double)M;
+    for (int o = 128; o > 0; o >>= 1) { if (t < o) { sh[t] += sh[t + o]; shc[t] += shc[t + o]; } __syncthreads(); }
+    const double Mw = shc[0];
+    const double mean = sh[0] / Mw;
     __syncthreads();
     double q = 0.0;
     for (int b = t; b < nblk; b += 256) {
-        const int cnt = min(BM, M - b * BM);
+        const double w = blk_weight(gw, grows, b);
+        const double cnt = (double)min(BM, M - b * BM) * w;
         const double dm = (double)ws[(size_t)b * 2 * N + n] - mean;
-        q += (double)ws[(size_t)b * 2 * N + N + n] + (double)cnt * dm * dm;
+        q += w * (double)ws[(size_t)b * 2 * N + N + n] + cnt * dm * dm;
     }
     sh[t] = q;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) { if (t < o) sh[t] += sh[t + o]; __syncthreads(); }
     if (t == 0) {
         const double m2 = sh[0];
-        const double var = m2 / (double)M;
+        const double var = m2 / Mw;
         const float is = (float)(1.0 / sqrt(var + (double)eps));
         const float mf = (float)mean;
         mean_o[n] = mf;
@@ -1002,7 +1015,7 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
         shift_o[n] = (beta ? beta[n] : 0.f) - mf * sc;
         if (running_mean) running_mean[n] = (1.f - momentum) * running_mean[n] + momentum * mf;
         if (running_var) {
-            const float uv = (float)(M > 1 ? m2 / (double)(M - 1) : m2);
+            const float uv = (float)(Mw > 1.0 ? m2 / (Mw - 1.0) : m2);
             running_var[n] = (1.f - momentum) * running_var[n] + momentum * uv;
         }
     }
@@ -1010,42 +1023,49 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
 
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ ws, int M, int N,
         const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma, float* dbeta, int accumulate,
-        float* ca, float* cb, float* cc) {
-    __shared__ double s1[256], s2[256];
+        float* ca, float* cb, float* cc, const float* __restrict__ gw, int grows) {
+    // the partials are sums over stored rows of the (already multiplicity-summed) gradient, so
+    // only the batch size M becomes the weighted row count
+    __shared__ double s1[256], s2[256], s3[256];
     const int n = blockIdx.x, t = threadIdx.x;
     const int nblk = (M + BM - 1) / BM;
-    double a = 0.0, b = 0.0;
+    double a = 0.0, b = 0.0, c = 0.0;
     for (int k = t; k < nblk; k += 256) {
         a += (double)ws[(size_t)k * 2 * N + n];
         b += (double)ws[(size_t)k * 2 * N + N + n];
+        c += (double)min(BM, M - k * BM) * blk_weight(gw, grows, k);
     }
-    s1[t] = a; s2[t] = b;
+    s1[t] = a; s2[t] = b; s3[t] = c;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
-        if (t < o) { s1[t] += s1[t + o]; s2[t] += s2[t + o]; }
+        if (t < o) { s1[t] += s1[t + o]; s2[t] += s2[t + o]; s3[t] += s3[t + o]; }
         __syncthreads();
     }
     if (t == 0) {
         const double db = s1[0], dg = s2[0];
+        const double Mw = s3[0];
         if (dbeta) dbeta[n] = accumulate ? dbeta[n] + (float)db : (float)db;
         if (dgamma) dgamma[n] = accumulate ? dgamma[n] + (float)dg : (float)dg;
         const double is = invstd[n];
         const double k = (gamma ? (double)gamma[n] : 1.0) * is;
         ca[n] = (float)k;
-        cb[n] = (float)(-k * is * dg / (double)M);
-        cc[n] = (float)(-k * db / (double)M);
+        cb[n] = (float)(-k * is * dg / Mw);
+        cc[n] = (float)(-k * db / Mw);
     }
 }
 
 // rows in blocks of 128 (matches the partial layout), 256 threads = columns
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ G, const float* __restrict__ Y,
         int M, int N, int ld, int res, const float* __restrict__ mean, const float* __restrict__ ca,
-        const float* __restrict__ cb, const float* __restrict__ cc, float* __restrict__ dY, float* __restrict__ colsum) {
+        const float* __restrict__ cb, const float* __restrict__ cc, float* __restrict__ dY, float* __restrict__ colsum,
+        const float* __restrict__ gw, int grows) {
     const int n = blockIdx.x * 256 + threadIdx.x;
     const int blk = blockIdx.y;
     if (n >= N) return;
-    const float a = ca[n], b = cb[n], c = cc[n], mu = mean[n];
     const int r0 = blk * BM, r1 = min(M, r0 + BM);
+    // a stored row standing for w identical batch rows carries w times the batch-mean terms
+    const float w = gw ? gw[r0 / grows] : 1.f;
+    const float a = ca[n], b = cb[n] * w, c = cc[n] * w, mu = mean[n];
     float s = 0.f;
     for (int r = r0; r < r1; ++r) {
         const size_t e = (size_t)r * ld + n;
@@ -1064,16 +1084,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
 // wave, 8 rows in flight per lane; the 4 row lanes' column sums combine in LDS in fixed order.
 __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restrict__ G, const float* __restrict__ Y,
         int M, int N, int ld, int res, const float* __restrict__ mean, const float* __restrict__ ca,
-        const float* __restrict__ cb, const float* __restrict__ cc, float* __restrict__ dY, float* __restrict__ colsum) {
+        const float* __restrict__ cb, const float* __restrict__ cc, float* __restrict__ dY, float* __restrict__ colsum,
+        const float* __restrict__ gw, int grows) {
     __shared__ float4 part[4][64];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int n = (blockIdx.x * 64 + tx) * 4;
     const int blk = blockIdx.y;
     const bool nv = n < N;
     const int nn = nv ? n : 0;
-    const float4 a = *reinterpret_cast<const float4*>(ca + nn), b = *reinterpret_cast<const float4*>(cb + nn);
-    const float4 c = *reinterpret_cast<const float4*>(cc + nn), mu = *reinterpret_cast<const float4*>(mean + nn);
     const int r0 = blk * BM, r1 = min(M, r0 + BM);
+    const float w = gw ? gw[r0 / grows] : 1.f;   // row multiplicity (see bn_bwd_apply_kernel)
+    const float4 a = *reinterpret_cast<const float4*>(ca + nn);
+    float4 b = *reinterpret_cast<const float4*>(cb + nn), c = *reinterpret_cast<const float4*>(cc + nn);
+    b.x *= w; b.y *= w; b.z *= w; b.w *= w;
+    c.x *= w; c.y *= w; c.z *= w; c.w *= w;
+    const float4 mu = *reinterpret_cast<const float4*>(mean + nn);
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     auto one = [&](float y, float g, float av, float bv, float cv, float m) {
         const float p = res ? fmaxf(y, 0.f) : y;
@@ -1317,45 +1342,53 @@ int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, in
 
 int ured_bn_fwd_finalize(const float* stat_ws, int M, int N, const float* gamma, const float* beta,
                          float eps, float momentum, float* running_mean, float* running_var,
-                         float* mean, float* invstd, float* scale, float* shift, void* stream) {
+                         float* mean, float* invstd, float* scale, float* shift,
+                         const float* group_w, int group_rows, void* stream) {
     ured::clear_error();
     URED_REQUIRE(M > 0 && N >= 0, "ured_bn_fwd_finalize: bad sizes M=%d N=%d", M, N);
     if (N == 0) return 0;
     URED_REQUIRE(stat_ws && mean && invstd && scale && shift, "ured_bn_fwd_finalize: null pointer");
+    URED_REQUIRE(!group_w || (group_rows > 0 && group_rows % BM == 0),
+                 "ured_bn_fwd_finalize: row weights need group_rows multiple of %d (got %d)", BM, group_rows);
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, stat_ws, M, N, gamma, beta,
-                       eps, momentum, running_mean, running_var, mean, invstd, scale, shift);
+                       eps, momentum, running_mean, running_var, mean, invstd, scale, shift, group_w, group_rows);
     return ured::launch_status("ured_bn_fwd_finalize");
 }
 
 int ured_bn_bwd_finalize(const float* bwd_ws, int M, int N, const float* gamma, const float* invstd,
                          float* dgamma, float* dbeta, int accumulate,
-                         float* coef_a, float* coef_b, float* coef_c, void* stream) {
+                         float* coef_a, float* coef_b, float* coef_c,
+                         const float* group_w, int group_rows, void* stream) {
     ured::clear_error();
     URED_REQUIRE(M > 0 && N >= 0, "ured_bn_bwd_finalize: bad sizes");
     if (N == 0) return 0;
     URED_REQUIRE(bwd_ws && invstd && coef_a && coef_b && coef_c, "ured_bn_bwd_finalize: null pointer");
+    URED_REQUIRE(!group_w || (group_rows > 0 && group_rows % BM == 0),
+                 "ured_bn_bwd_finalize: row weights need group_rows multiple of %d (got %d)", BM, group_rows);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, bwd_ws, M, N, gamma, invstd,
-                       dgamma, dbeta, accumulate, coef_a, coef_b, coef_c);
+                       dgamma, dbeta, accumulate, coef_a, coef_b, coef_c, group_w, group_rows);
     return ured::launch_status("ured_bn_bwd_finalize");
 }
 
 int ured_bn_bwd_apply(const float* G, const float* Y, int M, int N, int ld, int res,
                       const float* mean, const float* coef_a, const float* coef_b, const float* coef_c,
-                      float* dY, float* colsum_ws, void* stream) {
+                      float* dY, float* colsum_ws, const float* group_w, int group_rows, void* stream) {
     ured::clear_error();
     URED_REQUIRE(M >= 0 && N >= 0 && ld >= N, "ured_bn_bwd_apply: bad sizes");
     if (M == 0 || N == 0) return 0;
     URED_REQUIRE(G && Y && mean && coef_a && coef_b && coef_c && dY, "ured_bn_bwd_apply: null pointer");
+    URED_REQUIRE(!group_w || (group_rows > 0 && group_rows % BM == 0),
+                 "ured_bn_bwd_apply: row weights need group_rows multiple of %d (got %d)", BM, group_rows);
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (N % 4 == 0 && ld % 4 == 0 && al16(G) && al16(Y) && al16(dY) && al16(mean) && al16(coef_a) &&
         al16(coef_b) && al16(coef_c) && (!colsum_ws || al16(colsum_ws))) {
         dim3 grid((N / 4 + 63) / 64, (M + BM - 1) / BM);
         hipLaunchKernelGGL(bn_bwd_apply4_kernel, grid, dim3(256), 0, (hipStream_t)stream, G, Y, M, N, ld, res, mean,
-                           coef_a, coef_b, coef_c, dY, colsum_ws);
+                           coef_a, coef_b, coef_c, dY, colsum_ws, group_w, group_rows);
     } else {
         dim3 grid((N + 255) / 256, (M + BM - 1) / BM);
         hipLaunchKernelGGL(bn_bwd_apply_kernel, grid, dim3(256), 0, (hipStream_t)stream, G, Y, M, N, ld, res, mean,
-                           coef_a, coef_b, coef_c, dY, colsum_ws);
+                           coef_a, coef_b, coef_c, dY, colsum_ws, group_w, group_rows);
     }
     return ured::launch_status("ured_bn_bwd_apply");
 }

@@ -22,7 +22,9 @@ import torch
 class GraphedStep:
     def __init__(self, inner, example_batch, warmup=3):
         self.inner = inner
-        self.static = {k: v.clone() for k, v in example_batch.items()}
+        # tensors only: a UniqueRows entry (data-dependent shapes) cannot live in static buffers,
+        # so the graphed step encodes every source slot
+        self.static = {k: v.clone() for k, v in example_batch.items() if torch.is_tensor(v)}
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):   # warm-up: library loads, allocator, hipBLASLt workspaces
@@ -49,8 +51,8 @@ class GraphedStep:
         return self.inner.optimizer
 
     def step(self, batch, epoch=0):
-        for k, v in batch.items():
-            self.static[k].copy_(v, non_blocking=True)
+        for k, v in self.static.items():
+            v.copy_(batch[k], non_blocking=True)
         self.g_fwd_bwd.replay()
         self.inner.reduce_gradients()
         self.g_update.replay()

@@ -41,7 +41,8 @@ from network.deformation_net import re_residual_net  # noqa: E402
 from network.simple_encoder import TargetEncoder as simple_encoder  # noqa: E402
 from train_utils.load_sources import load_sources  # noqa: E402
 from train_utils.optimizer_dm import define_optimizer_dm_re_recon  # noqa: E402
-from ured_hip.ops import build_parts, part_aabb, segment_sum  # noqa: E402
+from ured_hip.kernels import RowWeights  # noqa: E402
+from ured_hip.ops import UniqueRows, build_parts, part_aabb, segment_sum  # noqa: E402
 
 MODULE_NAMES = ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "re_residual_net_full",
                 "src_encoder_all", "recon_decoder_src", "embedding_layer")
@@ -126,9 +127,24 @@ class TrainStep:
             src_sem_f = emb(src_sem_idx)
             tgt_sem_f = emb(batch["tgt_sem"])
         src_points = get_source_points(src_labels, self.db)
-        codes, src_pp = M["src_encoder_all"].forward_pointmajor(src_points, src_sem_f)
-        recon_src_p = M["recon_decoder_src"].forward_split(src_pp, codes, code_first=True,
-                                                           group_rows=self.np_per_part).view(B, P, -1, 3)
+        uq = batch.get("src_unique") if cfg.get("unique_sources", True) else None
+        if uq is not None:
+            # unique source encoding: the slots' inputs are functions of their source part
+            # only, so the encoder and recon_decoder_src run once per distinct part with row
+            # multiplicities (BN statistics / backward of the full batch), then expand
+            rw = RowWeights(uq.w, self.np_per_part)
+            with torch.no_grad():
+                sem_u = emb(self.db.sem[uq.uniq])
+            code_u, pp_u = M["src_encoder_all"].forward_pointmajor(self.db.points[uq.uniq].unsqueeze(0),
+                                                                   sem_u.unsqueeze(0), rw=rw)
+            rec_u = M["recon_decoder_src"].forward_split(pp_u, code_u, code_first=True,
+                                                         group_rows=self.np_per_part, rw=rw)
+            codes = uq.expand(code_u)
+            recon_src_p = uq.expand(rec_u.view(uq.U, -1)).view(B, P, -1, 3)
+        else:
+            codes, src_pp = M["src_encoder_all"].forward_pointmajor(src_points, src_sem_f)
+            recon_src_p = M["recon_decoder_src"].forward_split(src_pp, codes, code_first=True,
+                                                               group_rows=self.np_per_part).view(B, P, -1, 3)
         tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
         target_part_f, _, re_in, mask_part, part_x, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
         recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
@@ -193,10 +209,17 @@ class TrainStep:
                 "embedding_layer": m["embedding_layer"].state_dict()}
 
 
-def batch_to_device(b, device):
-    return {"x": torch.as_tensor(b["x"]).to(device), "labels": torch.as_tensor(b["labels"]).to(device),
-            "tgt_sem": torch.as_tensor(b["tgt_sem"]).to(device),
-            "src_labels": torch.as_tensor(b["src_labels"]).to(device)}
+def batch_to_device(b, device, num_sources=None):
+    """Host batch -> device tensors. With num_sources (the source DB size) the distinct source
+    parts of the batch are also computed here, on the host labels (UniqueRows; used by
+    TrainStep unless cfg["unique_sources"] is False). Left out for HIP-graph replay, whose
+    static buffers need fixed shapes."""
+    out = {"x": torch.as_tensor(b["x"]).to(device), "labels": torch.as_tensor(b["labels"]).to(device),
+           "tgt_sem": torch.as_tensor(b["tgt_sem"]).to(device),
+           "src_labels": torch.as_tensor(b["src_labels"]).to(device)}
+    if num_sources is not None:
+        out["src_unique"] = UniqueRows(b["src_labels"], num_sources, device)
+    return out
 
 
 class SyntheticLoader:
@@ -214,7 +237,7 @@ class SyntheticLoader:
             b = synthetic.make_batch(self.cfg["batch_size"], self.cfg.get("num_points", 2048), self.ns,
                                      max_parts=self.cfg["MAX_NUM_PARTS"], parts=self.cfg.get("parts", 4),
                                      seed=self.seed * 100003 + i)
-            yield batch_to_device(b, self.device)
+            yield batch_to_device(b, self.device, None if self.cfg.get("cuda_graph") else self.ns)
 
 
 class _ScalarLog:

@@ -74,8 +74,11 @@ class TargetEncoder(nn.Module):
         params += [self.per_point_out[3].weight, self.per_point_out[3].bias, self.fc.weight, self.fc.bias]
         return [bn for _, bn in convs], params
 
-    def forward_pointmajor(self, x, sem_f):
-        """-> code [G, C], per_point [G*n, C] (point-major)."""
+    def forward_pointmajor(self, x, sem_f, rw=None):
+        """-> code [G, C], per_point [G*n, C] (point-major).
+
+        rw: optional ured_hip.kernels.RowWeights for a unique-row batch (is_src: x holds the
+        distinct source parts, rw.w[g] = how many slots of the full batch part g fills)."""
         if self.is_src:
             B, P, n, _ = x.shape
             xf = x.reshape(B * P * n, 3)
@@ -87,7 +90,7 @@ class TargetEncoder(nn.Module):
             sem = sem_f.reshape(B * n, -1)
             spec_mode = "tgt"
         bns, params = self._layers()
-        spec = EncoderSpec(spec_mode, n, self.training, bns)
+        spec = EncoderSpec(spec_mode, n, self.training, bns, rw=rw)
         code, pp = PointEncoderFn.apply(spec, xf.float(), sem.float(), *params)
         return code, pp
 

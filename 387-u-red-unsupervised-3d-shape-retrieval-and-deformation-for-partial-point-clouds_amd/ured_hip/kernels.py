@@ -31,9 +31,9 @@ class GemmDesc(ctypes.Structure):
 _SIGS = {
     "ured_gemm": [ctypes.POINTER(GemmDesc), _P],
     "ured_splitk_reduce": [_P, _I, _I, _I, _P, _I, _I, _P],
-    "ured_bn_fwd_finalize": [_P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P],
-    "ured_bn_bwd_finalize": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P],
-    "ured_bn_bwd_apply": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "ured_bn_fwd_finalize": [_P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "ured_bn_bwd_finalize": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P],
+    "ured_bn_bwd_apply": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "ured_pool_finalize": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_group_colsum": [_P, _I, _I, _P, _I, _I, _P, _I, _P],
     "ured_group_colsum_split": [_P, _I, _I, _P, _I, _I, _I, _P, _P, _I, _P],
@@ -88,14 +88,29 @@ class BNState:
         self.mean, self.invstd, self.scale, self.shift = mean, invstd, scale, shift
 
 
-def bn_fwd_finalize(stat_ws, M, N, gamma, beta, eps, momentum, running_mean, running_var):
+class RowWeights:
+    """Row multiplicities of a unique-row batch: stored row r of group r // group_rows stands
+    for w[group] identical rows of the full batch (w float32 [G] on the device)."""
+    __slots__ = ("w", "group_rows")
+
+    def __init__(self, w, group_rows):
+        assert group_rows % BM == 0, "row weights need whole 128-row blocks per group"
+        self.w, self.group_rows = w.float().contiguous(), int(group_rows)
+
+
+def _rw(rw):
+    return (None, 0) if rw is None else (rw.w.data_ptr(), rw.group_rows)
+
+
+def bn_fwd_finalize(stat_ws, M, N, gamma, beta, eps, momentum, running_mean, running_var, rw=None):
     dev = stat_ws.device
     mean = torch.empty(N, device=dev)
     invstd = torch.empty(N, device=dev)
     scale = torch.empty(N, device=dev)
     shift = torch.empty(N, device=dev)
     _lib.call("ured_bn_fwd_finalize", _p(stat_ws), int(M), int(N), _p(gamma), _p(beta), float(eps), float(momentum),
-              _p(running_mean), _p(running_var), _p(mean), _p(invstd), _p(scale), _p(shift), _lib.stream_of(stat_ws))
+              _p(running_mean), _p(running_var), _p(mean), _p(invstd), _p(scale), _p(shift), *_rw(rw),
+              _lib.stream_of(stat_ws))
     return BNState(mean, invstd, scale, shift)
 
 
@@ -105,20 +120,20 @@ def bn_eval_state(gamma, beta, running_mean, running_var, eps):
     return BNState(running_mean.clone(), invstd, scale, beta - running_mean * scale)
 
 
-def bn_bwd_finalize(bwd_ws, M, N, gamma, invstd, dgamma, dbeta):
+def bn_bwd_finalize(bwd_ws, M, N, gamma, invstd, dgamma, dbeta, rw=None):
     dev = bwd_ws.device
     ca, cb, cc = (torch.empty(N, device=dev) for _ in range(3))
     _lib.call("ured_bn_bwd_finalize", _p(bwd_ws), int(M), int(N), _p(gamma), _p(invstd), _p(dgamma), _p(dbeta), 0,
-              _p(ca), _p(cb), _p(cc), _lib.stream_of(bwd_ws))
+              _p(ca), _p(cb), _p(cc), *_rw(rw), _lib.stream_of(bwd_ws))
     return ca, cb, cc
 
 
-def bn_bwd_apply(G, Y, res, mean, coefs, want_colsum=True):
+def bn_bwd_apply(G, Y, res, mean, coefs, want_colsum=True, rw=None):
     M, N = Y.shape
     dY = torch.empty_like(Y)
     cs = torch.empty(nblocks(M), N, device=Y.device) if want_colsum else None
     _lib.call("ured_bn_bwd_apply", _p(G), _p(Y), int(M), int(N), int(N), int(bool(res)), _p(mean),
-              _p(coefs[0]), _p(coefs[1]), _p(coefs[2]), _p(dY), _p(cs), _lib.stream_of(Y))
+              _p(coefs[0]), _p(coefs[1]), _p(coefs[2]), _p(dY), _p(cs), *_rw(rw), _lib.stream_of(Y))
     return dY, cs
 
 

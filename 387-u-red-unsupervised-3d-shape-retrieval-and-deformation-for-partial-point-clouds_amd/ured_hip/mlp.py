@@ -27,12 +27,16 @@ class EncoderSpec:
     mode "src": x [G*group_rows, 3] with per-group semantics sem [G, S] (row bias)
     mode "tgt": x [M, 3] with per-point semantics sem [M, S] (extra K columns)
     bn_modules: the 7 BatchNorm1d modules (running stats updated in place when training)
+    rw: optional K.RowWeights — group g of the call stands for rw.w[g] identical groups of
+        the full batch (unique-row training: batch statistics and BN backward are those of
+        the expanded batch; the caller expands outputs and sums duplicate gradients)
     """
 
-    def __init__(self, mode, group_rows, training, bn_modules, momentum=0.1, eps=BN_EPS):
+    def __init__(self, mode, group_rows, training, bn_modules, momentum=0.1, eps=BN_EPS, rw=None):
         assert mode in ("src", "tgt")
         self.mode, self.group_rows, self.training = mode, group_rows, training
         self.bn_modules, self.momentum, self.eps = bn_modules, momentum, eps
+        self.rw = rw
 
 
 def _bn_state(spec, i, Yws, M, N, gamma, beta):
@@ -41,7 +45,7 @@ def _bn_state(spec, i, Yws, M, N, gamma, beta):
         if bnm.num_batches_tracked is not None:
             bnm.num_batches_tracked.add_(1)
         mom = bnm.momentum if bnm.momentum is not None else 0.0
-        return K.bn_fwd_finalize(Yws, M, N, gamma, beta, spec.eps, mom, bnm.running_mean, bnm.running_var)
+        return K.bn_fwd_finalize(Yws, M, N, gamma, beta, spec.eps, mom, bnm.running_mean, bnm.running_var, rw=spec.rw)
     return K.bn_eval_state(gamma, beta, bnm.running_mean, bnm.running_var, spec.eps)
 
 
@@ -151,8 +155,8 @@ class PointEncoderFn(Function):
             K.gemm(M, N, Cn, dY, Cn, Wn, Wn.shape[1], G_, N, b_kmajor=True, epi=K.EPI_BNBWD,
                    Yp=Y, ldy=N, bn=st, bwd_res=False, bwd_ws=bws, **kw)
             dgamma, dbeta = torch.empty(N, device=dev), torch.empty(N, device=dev)
-            coefs = K.bn_bwd_finalize(bws, M, N, gs[i], st.invstd, dgamma, dbeta)
-            dYi, cs = K.bn_bwd_apply(G_, Y, False, st.mean, coefs)
+            coefs = K.bn_bwd_finalize(bws, M, N, gs[i], st.invstd, dgamma, dbeta, rw=spec.rw)
+            dYi, cs = K.bn_bwd_apply(G_, Y, False, st.mean, coefs, rw=spec.rw)
             W = Ws[i]
             dW = torch.empty(W.shape, device=dev)
             if i == 0:
@@ -190,11 +194,12 @@ class ResidualNetFn(Function):
     params: W1,b1,g1,be1, W2,b2,g2,be2, W3,b3,g3,be3, W4,b4 (14 tensors).
     code_first: True when the input is cat(code, pp) (recon_decoder_src).
     grouping: gidx int32 [M] (row -> group) + off int32 [G+1], or fixed group_rows.
+    rw: optional K.RowWeights (fixed group_rows only), as in EncoderSpec.
     """
 
     @staticmethod
     def forward(ctx, spec, pp, code, *params):
-        code_first, gidx, off, group_rows, training, bn_modules = spec
+        code_first, gidx, off, group_rows, training, bn_modules, rw = spec
         pp = pp.contiguous()
         code = code.contiguous()
         M, Cp = pp.shape
@@ -230,7 +235,7 @@ class ResidualNetFn(Function):
                     bnm.num_batches_tracked.add_(1)
                 st = K.bn_fwd_finalize(sws, M, N, params[4 * i + 2], params[4 * i + 3], BN_EPS,
                                        bnm.momentum if bnm.momentum is not None else 0.0,
-                                       bnm.running_mean, bnm.running_var)
+                                       bnm.running_mean, bnm.running_var, rw=rw)
             else:
                 st = K.bn_eval_state(params[4 * i + 2], params[4 * i + 3], bnm.running_mean, bnm.running_var, BN_EPS)
             Ys.append(Y)
@@ -246,7 +251,7 @@ class ResidualNetFn(Function):
 
     @staticmethod
     def backward(ctx, dout):
-        code_first, gidx, off, group_rows, training, bn_modules = ctx.spec
+        code_first, gidx, off, group_rows, training, bn_modules, rw = ctx.spec
         states = ctx.states
         saved = ctx.saved_tensors
         pp, code = saved[:2]
@@ -276,8 +281,8 @@ class ResidualNetFn(Function):
             K.gemm(M, N, Cn, dY, Cn, Wn, Wn.shape[1], G_, N, b_kmajor=True, epi=K.EPI_BNBWD,
                    Yp=Y, ldy=N, bn=st, bwd_res=True, bwd_ws=bws)
             dgamma, dbeta = torch.empty(N, device=dev), torch.empty(N, device=dev)
-            coefs = K.bn_bwd_finalize(bws, M, N, params[4 * i + 2], st.invstd, dgamma, dbeta)
-            dYi, cs = K.bn_bwd_apply(G_, Y, True, st.mean, coefs)
+            coefs = K.bn_bwd_finalize(bws, M, N, params[4 * i + 2], st.invstd, dgamma, dbeta, rw=rw)
+            dYi, cs = K.bn_bwd_apply(G_, Y, True, st.mean, coefs, rw=rw)
             W = params[4 * i].reshape(params[4 * i].shape[0], -1)
             dW = torch.empty(W.shape, device=dev)
             if i == 0:

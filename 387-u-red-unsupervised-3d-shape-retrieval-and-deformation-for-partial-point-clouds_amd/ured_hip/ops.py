@@ -89,3 +89,51 @@ def part_aabb(parts):
     lo = torch.zeros(B * P, 3, device=flat.device).scatter_reduce(0, idx, flat, "amin", include_self=False)
     hi = torch.zeros(B * P, 3, device=flat.device).scatter_reduce(0, idx, flat, "amax", include_self=False)
     return torch.cat([(lo + hi) / 2.0, (hi - lo) / 2.0], 1).view(B, P, 6)
+
+
+class ExpandGroupsFn(Function):
+    """out[r] = xu[inverse[r]] — expands the distinct rows of a unique-row batch back to the
+    full batch. Backward sums the gradients of each distinct row's copies in a fixed order
+    (rows sorted by `order`, segment offsets `off`; HIP group_colsum): deterministic, unlike
+    index_select's atomic index_add backward."""
+
+    @staticmethod
+    def forward(ctx, xu, inverse, order, off):
+        ctx.save_for_backward(order, off)
+        ctx.U = xu.shape[0]
+        return xu.index_select(0, inverse)
+
+    @staticmethod
+    def backward(ctx, g):
+        order, off = ctx.saved_tensors
+        g = g.contiguous()
+        gs = g.reshape(g.shape[0], -1).index_select(0, order)
+        gu = K.group_colsum(gs, gs.shape[1], ctx.U, off=off)
+        return gu.view(ctx.U, *g.shape[1:]), None, None, None
+
+
+class UniqueRows:
+    """Distinct entries of a batch of source-part slots (engine/train.py:196-211: every slot
+    whose label is -1 — and any repeated label — encodes the same source part).
+
+    uniq [U] (db row of each distinct part), inverse [R] (distinct part of each slot),
+    order [R] (slots sorted by distinct part, stable), off int32 [U+1], w float32 [U] (copies).
+    Built on the host from the host-side labels (no device sync), then copied once.
+    """
+
+    def __init__(self, labels_host, num_sources, device):
+        import numpy as np
+        s = np.asarray(labels_host).reshape(-1).astype(np.int64)
+        idx = np.where(s < 0, s + num_sources, s)      # python negative indexing (dataset_utils.py:800-805)
+        uniq, inv, cnt = np.unique(idx, return_inverse=True, return_counts=True)
+        order = np.argsort(inv, kind="stable")
+        off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
+        self.U = int(uniq.shape[0])
+        self.uniq = torch.from_numpy(uniq).to(device)
+        self.inverse = torch.from_numpy(inv.reshape(-1).astype(np.int64)).to(device)
+        self.order = torch.from_numpy(order.astype(np.int64)).to(device)
+        self.off = torch.from_numpy(off).to(device)
+        self.w = torch.from_numpy(cnt.astype(np.float32)).to(device)
+
+    def expand(self, xu):
+        return ExpandGroupsFn.apply(xu, self.inverse, self.order, self.off)

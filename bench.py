@@ -178,6 +178,10 @@ def main():
                     help="replay the step as HIP graphs (engine/graph.py; N=1 unless --graph-dp). Measured "
                          "equal to eager once the step has no host syncs, so eager is the default")
     ap.add_argument("--graph-dp", action="store_true", help="HIP-graph replay also when N > 1")
+    ap.add_argument("--all-slots", action="store_true",
+                    help="encode every source slot (no unique-source encoding) in the timed run")
+    ap.add_argument("--no-all-slots-rate", action="store_true",
+                    help="skip the extra timed run that encodes every source slot")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -200,8 +204,10 @@ def main():
     cfg["cuda_graph"] = use_graph
     db, _ = load_sources(cfg, dev)
     eager = DataParallelStep(cfg, db, dev)
+    cfg["unique_sources"] = not args.all_slots
     batches = [batch_to_device(synthetic.make_batch(args.batch, args.points, db.num_sources, parts=args.parts,
-                                                    seed=1000 * rank + i), dev) for i in range(4)]
+                                                    seed=1000 * rank + i), dev,
+                               None if use_graph else db.num_sources) for i in range(4)]
     if use_graph:   # capture (after 3 eager warm-up steps on batch 0); replays below
         from engine.graph import GraphedStep
         step = GraphedStep(eager, batches[0])
@@ -227,6 +233,29 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     loss_val = float(T["all_loss"].item())
+
+    def timed_rate(steps):   # same protocol (barrier + sync both sides, max over ranks)
+        for i in range(2):
+            eager.step(batches[i % 4])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for i in range(steps):
+            eager.step(batches[i % 4])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tt = torch.tensor([time.perf_counter() - t1], device=dev)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return steps * world / float(tt.item())
+
+    all_slots_rate = None
+    if not args.no_all_slots_rate and cfg["unique_sources"] and not use_graph:
+        cfg["unique_sources"] = False      # every one of the B x 16 source slots encoded
+        all_slots_rate = timed_rate(args.steps)
+        cfg["unique_sources"] = True
 
     breakdown = None
     if not args.no_breakdown:
@@ -276,6 +305,9 @@ def main():
         extra["gemm_variants"] = {k: {"launches": round(v["launches"], 2), "ms": round(v["ms"], 3),
                                       "tflops": round(v["flop"] / max(v["ms"], 1e-9) / 1e9, 2)}
                                   for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
+    if all_slots_rate is not None:
+        extra["all_slots_iters_s"] = round(all_slots_rate, 4)
+    extra["unique_sources"] = bool(cfg["unique_sources"]) and not use_graph
     extra["chamfer_gpair_s"] = round(chamfer_rate(dev), 1)
     extra["pseudo_label_dcd"] = pair_rate(dev)
     extra["loss"] = loss_val

@@ -153,23 +153,31 @@ int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, in
 /* BN forward finalize over the per-block partials of EPI_FWD (M rows, blocks of 128):
  * fp64 Chan merge -> mean, invstd = 1/sqrt(var_biased+eps), scale = gamma*invstd,
  * shift = beta - mean*scale; running stats (if non-NULL) updated in place with
- * momentum and the unbiased variance (torch.nn.BatchNorm1d semantics). */
+ * momentum and the unbiased variance (torch.nn.BatchNorm1d semantics).
+ * Row multiplicities (unique-row training): if group_w is non-NULL, each stored row of
+ * group g = row / group_rows (group_rows a multiple of 128) stands for group_w[g] identical
+ * rows of the batch; statistics are those of the expanded batch (count sum_g w_g*rows_g).
+ * The same (group_w, group_rows) pair goes to the two backward calls below. */
 int ured_bn_fwd_finalize(const float* stat_ws, int M, int N, const float* gamma, const float* beta,
                          float eps, float momentum, float* running_mean, float* running_var,
-                         float* mean, float* invstd, float* scale, float* shift, void* stream);
+                         float* mean, float* invstd, float* scale, float* shift,
+                         const float* group_w, int group_rows, void* stream);
 
 /* BN backward finalize over EPI_BNBWD partials: dbeta = sum g, dgamma = sum g*xhat
  * (fp64, fixed order; written, or added if accumulate) and the coefficients of
  * dY = coef_a*g + coef_b*(p - mean) + coef_c (see ured_bn_bwd_apply). */
 int ured_bn_bwd_finalize(const float* bwd_ws, int M, int N, const float* gamma, const float* invstd,
                          float* dgamma, float* dbeta, int accumulate,
-                         float* coef_a, float* coef_b, float* coef_c, void* stream);
+                         float* coef_a, float* coef_b, float* coef_c,
+                         const float* group_w, int group_rows, void* stream);
 
 /* dY[m][n] = coef_a*g + coef_b*(p-mean) + coef_c with p = Y (ENC) or relu(Y) (RES, then
- * times (Y > 0)). Also writes per-128-row column partial sums of dY to colsum_ws[blk][N]. */
+ * times (Y > 0)). Also writes per-128-row column partial sums of dY to colsum_ws[blk][N].
+ * With group_w, G holds the multiplicity-summed gradient of each stored row and the
+ * mean terms are scaled by the row's weight: dY = coef_a*g + w*(coef_b*(p-mean) + coef_c). */
 int ured_bn_bwd_apply(const float* G, const float* Y, int M, int N, int ld, int res,
                       const float* mean, const float* coef_a, const float* coef_b, const float* coef_c,
-                      float* dY, float* colsum_ws, void* stream);
+                      float* dY, float* colsum_ws, const float* group_w, int group_rows, void* stream);
 
 /* Max-pool finalize (TargetEncoder max_pool1d over each group of group_rows points of
  * relu(scale*Y+shift)): pooled[g][n] and the winning row index argidx[g][n]. */

@@ -25,7 +25,7 @@ CFG = {"source_latent_dim": 64, "target_latent_dim": 64, "sem_latent_dim": 16, "
        "weight_decay": 5e-4, "lr_stepsize": 3, "lr_decay": 0.5, "momentum": 0.9}
 
 
-def _setup(dev, B=2, N=128, parts=(3, 2), ns=24, seed=4):
+def _setup(dev, B=2, N=128, parts=(3, 2), ns=24, seed=4, unique=True):
     from dataset import synthetic
     from train_utils.load_sources import SourceDB
     from engine.train import TrainStep, batch_to_device
@@ -37,7 +37,7 @@ def _setup(dev, B=2, N=128, parts=(3, 2), ns=24, seed=4):
     P = ured_ref.make_params(cfg, seed=7)
     for name, sd in P.items():
         ts.models[name].load_state_dict(sd, strict=True)
-    batch = batch_to_device(bt, dev)
+    batch = batch_to_device(bt, dev, ns if unique else None)
     ob = {"src_points": torch.from_numpy(db_np["src_points"]), "src_mats": torch.from_numpy(db_np["src_mats"]),
           "src_sem": torch.from_numpy(db_np["src_sem"]), "src_index": torch.from_numpy(bt["src_index"]),
           "tgt_sem": torch.from_numpy(bt["tgt_sem"]), "x": torch.from_numpy(bt["x"]),
@@ -63,9 +63,14 @@ TERMS = ("cd_loss_full", "cd_loss_part", "contrast_loss", "ref_cd_loss_full", "r
          "re_reg_loss_full", "reg_loss_full", "recon_loss_full", "recon_loss_src", "all_loss")
 
 
+@pytest.mark.parametrize("unique", [True, False], ids=["unique_sources", "all_slots"])
 @pytest.mark.parametrize("N,parts", [(128, (3, 2)), (512, (4, 4)), (256, (16, 1))])
-def test_train_step_matches_oracle(dev, N, parts):
-    ts, batch, P, ob, cfg = _setup(dev, N=N, parts=parts)
+def test_train_step_matches_oracle(dev, N, parts, unique):
+    """unique: the source encoder / recon_decoder_src run once per distinct source part with
+    row multiplicities (the oracle always encodes every slot, as the reference does)."""
+    ts, batch, P, ob, cfg = _setup(dev, N=N, parts=parts, unique=unique)
+    if unique:
+        assert batch["src_unique"].U < 2 * 16   # padding slots collapse onto one source part
     loss, T = ts.forward(batch)
     rloss, R = ured_ref.train_forward(P, ob, cfg)
     for k in TERMS:
@@ -107,3 +112,36 @@ def test_train_step_runs_and_updates(dev):
     assert torch.isfinite(T1["all_loss"]) and torch.isfinite(T2["all_loss"])
     assert not torch.equal(w0, ts.models["param_decoder_full"].param_decoder[2].weight.detach())
     assert int(ts.models["target_encoder_full"].mlp1[1].num_batches_tracked) == 2
+
+
+def test_unique_sources_equal_all_slots(dev):
+    """Unique-source encoding vs encoding all B x 16 slots on the GPU: same losses, gradients
+    and BN running statistics up to fp32 summation order."""
+    from engine.train import batch_to_device
+    ts1, b1, P, ob, cfg = _setup(dev, N=256, parts=(5, 2), unique=True)
+    ts2, b2, _, _, _ = _setup(dev, N=256, parts=(5, 2), unique=False)
+    assert "src_unique" in b1 and "src_unique" not in b2
+    l1, T1 = ts1.forward(b1)
+    l2, T2 = ts2.forward(b2)
+    for k in TERMS:
+        a, b = T1[k].item(), T2[k].item()
+        assert abs(a - b) <= 1e-5 * abs(b) + 1e-7, f"{k}: {a} vs {b}"
+    l1.backward()
+    l2.backward()
+    for name in ("src_encoder_all", "recon_decoder_src"):
+        m1, m2 = ts1.models[name], ts2.models[name]
+        p2 = dict(m2.named_parameters())
+        for k, p in m1.named_parameters():
+            if p.grad is None:
+                assert p2[k].grad is None
+                continue
+            if k in BN_FED_BIAS:
+                continue
+            d = (p.grad - p2[k].grad).norm().item()
+            assert d <= 2e-3 * p2[k].grad.norm().item() + 1e-5, f"{name}.{k}: |diff| {d}"
+        b2s = dict(m2.named_buffers())
+        for k, v in m1.named_buffers():
+            if v.dtype.is_floating_point:
+                assert torch.allclose(v, b2s[k], rtol=1e-4, atol=1e-6), f"{name}.{k}"
+            else:
+                assert torch.equal(v, b2s[k])
