@@ -1,13 +1,20 @@
 """Graph attention network of DeformNet_MatchingNet (reference attention_graph/attention_gnn.py:8-98).
 
-Module/attribute names match the reference so checkpoints interchange. The
-graph has 2 global + MAX_NUM_PARTS part nodes per sample: these are tiny,
-latency-bound ops and stay on torch (hipBLAS) kernels.
+Module/attribute names match the reference so checkpoints interchange. The graph has
+2 global + MAX_NUM_PARTS part nodes per sample: tiny, launch-bound work. The U-RED step
+runs it node-major (`forward_nodes`, [B, nodes, C]): q|k|v projections as one fused
+F.linear, the attention core as one HIP kernel each way (ured_hip.attn), so a message
+passing call is ~8 launches instead of ~20 with layout copies. `forward` keeps the
+reference's channel-first signature for drop-in callers.
 """
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
+
+from ured_hip.attn import cross_attention, self_attention
 
 from . import get_attention_mechanism
+from .attention import softmax_attention
 from .attention_utils import FeedForwardNet_norm, conv1x1
 
 
@@ -30,6 +37,25 @@ class MultiheadAttention(nn.Module):
                                        conv1x1(self.in_proj_v, value).view(split))
         return conv1x1(self.out_proj, out.reshape(b, self.num_heads * self.embed_dim, -1)), att
 
+    @staticmethod
+    def _w(conv):
+        return conv.weight.view(conv.weight.shape[0], -1)
+
+    def forward_nodes(self, xq, xkv=None):
+        """Node-major [B, n, C] query nodes and [B, m, C] key/value nodes (None: self-attention)
+        -> message [B, n, C]."""
+        if self.attention_func is not softmax_attention:
+            raise NotImplementedError("node-major path implements the softmax attention only")
+        q_, k_, v_ = self.in_proj_q, self.in_proj_k, self.in_proj_v
+        if xkv is None:
+            qkv = F.linear(xq, torch.cat([self._w(q_), self._w(k_), self._w(v_)]), torch.cat([q_.bias, k_.bias, v_.bias]))
+            out = self_attention(qkv, self.num_heads)
+        else:
+            q = F.linear(xq, self._w(q_), q_.bias)
+            kv = F.linear(xkv, torch.cat([self._w(k_), self._w(v_)]), torch.cat([k_.bias, v_.bias]))
+            out = cross_attention(q, kv, self.num_heads)
+        return F.linear(out, self._w(self.out_proj), self.out_proj.bias)
+
 
 class ResidualAttentionMessagePropagation(nn.Module):
     def __init__(self, embed_dim, num_heads, attention="softmax", use_offset=False, use_norm="use_bn"):
@@ -43,6 +69,11 @@ class ResidualAttentionMessagePropagation(nn.Module):
         first = desc_q - message if self.use_offset else desc_q
         return desc_q + self.fc(torch.cat([first, message], dim=1))
 
+    def forward_nodes(self, xq, xkv=None):
+        message = self.mha.forward_nodes(xq, xkv)
+        first = xq - message if self.use_offset else xq
+        return xq + self.fc.forward_nodes(torch.cat([first, message], dim=-1))
+
 
 class DescriptorsSelfAttention(nn.Module):
     def __init__(self, embed_dim, num_heads, attention="softmax", use_offset=False):
@@ -51,6 +82,9 @@ class DescriptorsSelfAttention(nn.Module):
 
     def forward(self, desc0, desc1):
         return self.module(desc0, desc0), self.module(desc1, desc1)
+
+    def forward_nodes(self, desc0, desc1):
+        return self.module.forward_nodes(desc0), self.module.forward_nodes(desc1)
 
 
 class DescriptorsCrossAttention(nn.Module):
@@ -61,6 +95,10 @@ class DescriptorsCrossAttention(nn.Module):
     def forward(self, desc0, desc1):
         desc0 = self.module(desc0, desc1)       # the updated desc0 feeds desc1's update
         return desc0, self.module(desc1, desc0)
+
+    def forward_nodes(self, desc0, desc1):
+        desc0 = self.module.forward_nodes(desc0, desc1)
+        return desc0, self.module.forward_nodes(desc1, desc0)
 
 
 class GraphAttentionNet(nn.Module):
@@ -74,4 +112,10 @@ class GraphAttentionNet(nn.Module):
     def forward(self, desc0, desc1):
         for layer in self.layers:
             desc0, desc1 = layer(desc0, desc1)
+        return desc0, desc1
+
+    def forward_nodes(self, desc0, desc1):
+        """Node-major [B, n0, C], [B, n1, C]."""
+        for layer in self.layers:
+            desc0, desc1 = layer.forward_nodes(desc0, desc1)
         return desc0, desc1

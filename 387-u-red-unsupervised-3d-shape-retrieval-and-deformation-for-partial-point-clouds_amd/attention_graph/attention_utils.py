@@ -32,6 +32,23 @@ def _ffn_layers(dims, use_norm):
 class FeedForwardNet_norm(nn.Sequential):
     def __init__(self, arg_list, use_norm="use_bn"):
         super().__init__(*_ffn_layers(list(arg_list), use_norm))
+        self.use_norm = use_norm
+
+    def forward_nodes(self, x):
+        """Same network on node-major x [B, n, Cin] -> [B, n, Cout]: each Conv1d(k=1) is one
+        F.linear (bias fused into the GEMM), BatchNorm1d sees the [B*n, C] rows (the same
+        per-channel batch statistics as on [B, C, n]); no layout copies."""
+        if self.use_norm not in ("use_bn", "None", None):
+            return self.forward(x.transpose(1, 2)).transpose(1, 2)
+        B, n, _ = x.shape
+        for layer in self:
+            if isinstance(layer, nn.Conv1d):
+                x = F.linear(x, layer.weight.view(layer.weight.shape[0], -1), layer.bias)
+            elif isinstance(layer, nn.ReLU):
+                x = F.relu(x)
+            else:
+                x = layer(x.reshape(B * n, -1)).view(B, n, -1)
+        return x
 
     def forward(self, x):
         for layer in self:

@@ -38,14 +38,15 @@ class DeformNet_MatchingNet(nn.Module):
                              if matching else None)
 
     def forward(self, target_f, src_part_f, per_point_f=None):
+        """Node-major throughout: the reference's [B, C, nodes] tensors are held as [B, nodes, C]
+        (same values; channel-first views are never materialised)."""
         bs = target_f.shape[0]
-        parts = src_part_f.reshape(bs, src_part_f.shape[1], -1).transpose(1, 2)      # [B, C, P]
-        nodes = torch.stack([parts.mean(dim=-1), target_f], dim=-1)                   # [B, C, 2]
-        nodes, parts = self.graph_attention_net(nodes, parts)
-        P = parts.shape[-1]
-        glob = nodes.transpose(1, 2).reshape(bs, -1, 1).expand(-1, -1, P)            # [g0 | g1] per part
-        out = self.param_decoder(torch.cat([glob, parts], dim=1))                      # [B, 6, P]
-        return out.transpose(1, 2).contiguous()
+        parts = src_part_f.reshape(bs, src_part_f.shape[1], -1)                        # [B, P, C]
+        nodes = torch.stack([parts.mean(dim=1), target_f], dim=1)                      # [B, 2, C]
+        nodes, parts = self.graph_attention_net.forward_nodes(nodes, parts)
+        P = parts.shape[1]
+        glob = nodes.reshape(bs, 1, -1).expand(-1, P, -1)                              # [g0 | g1] per part
+        return self.param_decoder.forward_nodes(torch.cat([glob, parts], dim=-1))      # [B, P, 6]
 
 
 class re_residual_net(nn.Module):

@@ -4,5 +4,6 @@
   nn       nearest-neighbour / chamfer autograd ops (dense + ragged segments)
   kernels  typed wrappers of the fused per-point MLP entry points
   mlp      PointEncoderFn / ResidualNetFn autograd chains
+  attn     graph-node multi-head attention (DeformNet's GraphAttentionNet core)
 """
-from . import _lib, kernels, nn  # noqa: F401
+from . import _lib, attn, kernels, nn  # noqa: F401

@@ -198,6 +198,25 @@ int ured_group_colsum(const float* X, int ldx, int N, const int* off, int group_
 int ured_group_colsum_split(const float* X, int ldx, int N, const int* off, int group_rows, int G, int splits,
                             float* ws, float* out, int ldo, void* stream);
 
+/* ---------------- graph attention (DeformNet_MatchingNet) ---------------- */
+
+/* Multi-head softmax attention over graph nodes, node-major layout
+ * (replaces attention_graph/attention.py:8-19 as called by attention_gnn.py:20-32).
+ * Row r of sample b: q + (b*n + r)*ldq, k/v + (b*m + r)*ld{k,v}; head h occupies columns
+ * [h*d, (h+1)*d) (the reference's view(B, H, d, nodes) channel split).
+ *   weights[b][h][i][j] = softmax_j(scale * <q_bi^h, k_bj^h>),  out_bi^h = sum_j weights * v_bj^h
+ * weights [B*H*n*m] is written by the forward and read by the backward, which overwrites
+ * dq [B,n,*], dk/dv [B,m,*] (may be column slices of one buffer). Limits: n, m <= 32,
+ * d <= 128, and the (n, m, d) LDS image within 64 KB. */
+#define URED_ATTN_MAX_NODES 32
+#define URED_ATTN_MAX_HEAD_DIM 128
+int ured_attn_fwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv,
+                  int B, int H, int n, int m, int d, float scale, float* out, int ldo, float* weights,
+                  void* stream);
+int ured_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv, const float* weights,
+                  const float* dout, int lddo, int B, int H, int n, int m, int d, float scale,
+                  float* dq, int lddq, float* dk, int lddk, float* dv, int lddv, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

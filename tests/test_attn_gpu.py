@@ -1,0 +1,119 @@
+"""Graph-node attention kernel (ured_attn_fwd/bwd) and the node-major DeformNet path.
+
+* the fused self / cross attention vs a float64 torch restatement of the reference's
+  softmax_attention (attention_graph/attention.py:8-19): outputs and q/k/v gradients
+  within 1e-5 relative;
+* DeformNet_MatchingNet.forward (node-major, HIP attention) vs the same module run
+  channel-first through its reference-layout submodules (torch ops only): params and
+  every parameter gradient within 1e-5 relative, same BN running statistics.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_attn(q, k, v, H):
+    """Reference semantics on node-major inputs: view(B, H, d, n) of the channel-first tensor."""
+    B, n, C = q.shape
+    m = k.shape[1]
+    d = C // H
+    qh = q.view(B, n, H, d).permute(0, 2, 1, 3)
+    kh = k.view(B, m, H, d).permute(0, 2, 1, 3)
+    vh = v.view(B, m, H, d).permute(0, 2, 1, 3)
+    w = (qh @ kh.transpose(-1, -2) * d ** -0.5).softmax(-1)
+    return (w @ vh).permute(0, 2, 1, 3).reshape(B, n, C)
+
+
+def _close(a, b, rtol=1e-5):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    assert (a - b).abs().max().item() <= rtol * b.abs().max().item() + 1e-7, (a - b).abs().max().item()
+
+
+@pytest.mark.parametrize("B,H,n,m,d", [(16, 4, 2, 16, 128), (16, 4, 16, 2, 128), (3, 2, 5, 7, 16), (2, 4, 32, 32, 8)])
+def test_cross_attention_matches_reference(dev, B, H, n, m, d):
+    from ured_hip.attn import cross_attention
+    g = torch.Generator().manual_seed(n * 31 + m)
+    C = H * d
+    q = torch.randn(B, n, C, generator=g)
+    kv = torch.randn(B, m, 2 * C, generator=g)
+    go = torch.randn(B, n, C, generator=g)
+    qd, kvd = q.to(dev).requires_grad_(True), kv.to(dev).requires_grad_(True)
+    out = cross_attention(qd, kvd, H)
+    out.backward(go.to(dev))
+    qr, kvr = q.double().requires_grad_(True), kv.double().requires_grad_(True)
+    ref = _ref_attn(qr, kvr[..., :C], kvr[..., C:], H)
+    ref.backward(go.double())
+    _close(out, ref)
+    _close(qd.grad, qr.grad)
+    _close(kvd.grad, kvr.grad)
+
+
+@pytest.mark.parametrize("B,H,n,d", [(16, 4, 16, 128), (16, 4, 2, 128), (2, 3, 9, 5)])
+def test_self_attention_matches_reference(dev, B, H, n, d):
+    from ured_hip.attn import self_attention
+    g = torch.Generator().manual_seed(n + d)
+    C = H * d
+    qkv = torch.randn(B, n, 3 * C, generator=g)
+    go = torch.randn(B, n, C, generator=g)
+    x = qkv.to(dev).requires_grad_(True)
+    out = self_attention(x, H)
+    out.backward(go.to(dev))
+    xr = qkv.double().requires_grad_(True)
+    ref = _ref_attn(xr[..., :C], xr[..., C:2 * C], xr[..., 2 * C:], H)
+    ref.backward(go.double())
+    _close(out, ref)
+    _close(x.grad, xr.grad)
+
+
+def test_attention_rejects_oversize(dev):
+    from ured_hip import _lib
+    from ured_hip.attn import cross_attention
+    with pytest.raises(_lib.UredError, match="exceed"):
+        cross_attention(torch.zeros(1, 40, 8, device=dev), torch.zeros(1, 3, 16, device=dev), 1)
+
+
+def _channel_first_forward(net, target_f, src_part_f):
+    """deformation_net.py:74-93 verbatim in layout, on this module's reference-layout
+    (channel-first, torch-op) submodule forwards."""
+    bs = target_f.shape[0]
+    P = src_part_f.shape[1]
+    parts = src_part_f.view(bs, P, -1).permute(0, 2, 1)
+    nodes = torch.cat([parts.mean(dim=-1).unsqueeze(-1), target_f.unsqueeze(-1)], dim=-1)
+    ga, pa = net.graph_attention_net(nodes, parts)
+    gr = torch.cat([ga[:, :, 0], ga[:, :, 1]], dim=1).view(bs, -1, 1).repeat(1, 1, P)
+    return net.param_decoder(torch.cat([gr, pa], dim=1)).permute(0, 2, 1).contiguous()
+
+
+@pytest.mark.parametrize("C", [64, 512])
+def test_deformnet_node_major_equals_channel_first(dev, C):
+    import copy
+    from network.deformation_net import DeformNet_MatchingNet
+    torch.manual_seed(C)
+    net = DeformNet_MatchingNet(3 * C, graph_dim=C, max_num_parts=16, matching=False).to(dev).train()
+    ref = copy.deepcopy(net)
+    tf = torch.randn(16, C, device=dev)
+    sp = torch.randn(16, 16, C, device=dev)
+    a_t, a_s = tf.clone().requires_grad_(True), sp.clone().requires_grad_(True)
+    b_t, b_s = tf.clone().requires_grad_(True), sp.clone().requires_grad_(True)
+    out = net(a_t, a_s, None)
+    rout = _channel_first_forward(ref, b_t, b_s)
+    assert out.shape == (16, 16, 6)
+    _close(out, rout, 1e-4)
+    go = torch.randn_like(out)
+    out.backward(go)
+    rout.backward(go)
+    _close(a_t.grad, b_t.grad, 1e-4)
+    _close(a_s.grad, b_s.grad, 1e-4)
+    rp = dict(ref.named_parameters())
+    for k, p in net.named_parameters():
+        if p.grad is None:
+            assert rp[k].grad is None, k
+            continue
+        _close(p.grad, rp[k].grad, 1e-4)
+    rb = dict(ref.named_buffers())
+    for k, v in net.named_buffers():
+        if v.dtype.is_floating_point:
+            _close(v, rb[k], 1e-5)
+        else:
+            assert torch.equal(v, rb[k]), k

@@ -141,6 +141,11 @@ def synthetic_step_batch():
     return batch
 
 
+_ENC_BN_FED = ("mlp1.0", "mlp1.3", "mlp2.0", "mlp2.3", "mlp2.6", "fuse_sem.0", "per_point_out.0")
+_RES_BN_FED = ()    # Conv -> ReLU -> BN: the ReLU keeps the conv bias gradient non-trivial
+BN_FED = {"src_encoder_all": _ENC_BN_FED, "target_encoder_full": _ENC_BN_FED}
+
+
 def test_train_step_golden():
     """The whole engine/train.py:204-338 step (reference functions composed) vs the oracle."""
     g = _g("train_step.npz")
@@ -165,10 +170,15 @@ def test_train_step_golden():
         got = P[mod][name].grad
         assert got is not None, key
         # conv biases that feed a training-mode BN have ~0 true gradient (BN cancels them):
-        # their norms are rounding noise, hence the absolute floor
+        # their norms are rounding noise (platform-dependent: BLAS blocking / threads), so
+        # they are only bounded relative to the layer's weight gradient
+        if name.endswith(".bias") and name.replace(".bias", "") in BN_FED.get(mod, ()):
+            wn = P[mod][name.replace(".bias", ".weight")].grad.norm().item()
+            assert got.norm().item() <= 1e-2 * wn + 1e-4 and g[key] <= 1e-2 * wn + 1e-4, key
+            continue
         np.testing.assert_allclose(got.norm().item(), g[key], rtol=2e-3, atol=1e-4, err_msg=key)
         nchecked += 1
-    assert nchecked > 150
+    assert nchecked > 130
     np.testing.assert_allclose(P["param_decoder_full"]["param_decoder.2.weight"].grad.numpy(),
                                g["g/param_decoder.2.weight"], rtol=2e-3, atol=1e-5)
     np.testing.assert_allclose(P["recon_decoder_src"]["residual_net.9.weight"].grad.numpy(),

@@ -30,7 +30,8 @@ def main():
     dev = torch.device("cuda:0")
     db, _ = load_sources(cfg, dev)
     step = DataParallelStep(cfg, db, dev)
-    batches = [batch_to_device(synthetic.make_batch(16, 2048, db.num_sources, parts=4, seed=i), dev) for i in range(2)]
+    batches = [batch_to_device(synthetic.make_batch(16, 2048, db.num_sources, parts=4, seed=i), dev, db.num_sources)
+               for i in range(2)]
     for i in range(3):
         step.step(batches[i % 2])
     torch.cuda.synchronize()
