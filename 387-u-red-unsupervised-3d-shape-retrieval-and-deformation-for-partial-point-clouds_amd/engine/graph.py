@@ -1,46 +1,57 @@
 """The training step as HIP graphs (torch.cuda.CUDAGraph = hipGraph on ROCm).
 
-One eager step issues ~1400 kernel launches (the fused HIP GEMMs plus many small torch ops of
-DeformNet, the losses and the optimizer); their host-side launch cost leaves the GPU idle for
-several ms per step. The step has static shapes and no host sync (segment tables and part
-pooling are built on device), so it is captured once and replayed:
+An eager step issues ~1000 kernel launches (the fused HIP GEMMs plus the small torch ops of
+the losses, DeformNet's projections and the optimizer) through Python, ctypes and the
+autograd engine; at ~20 ms of GPU work per step that host cost is the same order as the GPU
+time. The step has no host sync (segment tables, part pooling and the unique-source tables
+are built on the device or from host labels before the step), so it is captured and replayed:
 
-  graph 1: zero_grad + forward + backward      (our ctypes launches go to torch's current
-                                                 stream, i.e. the capture stream)
-  eager  : reduce_gradients()                   (RCCL bucketed all-reduce when world > 1)
-  graph 2: clip_grad_norm_ x6 + Adam            (Adam built with capturable=True)
+  graph "fwd_bwd"[key] : grads.zero_() + forward + backward
+  eager                : reduce_gradients()      (RCCL bucketed all-reduce when world > 1)
+  graph "update"       : clip_grad_norm_ x6 + Adam (capturable)
 
-Inputs are copied into static buffers before each replay; the returned loss dict holds the
-graph's static output tensors (valid until the next replay). Same kernels, same arithmetic
-as the eager step: a replay is bit-identical to an eager step on the same state and batch.
-With world > 1 the forward contains the contrastive loss's all_gather; graph mode is then
-opt-in (cfg["cuda_graph_dp"]), the default keeps the eager path.
+key = the batch's padded distinct-source-part count (UniqueRows with a bucket; None when the
+batch encodes every slot): one forward/backward graph per key, captured the first time the key
+is seen, right after that batch's step runs eagerly (so no extra optimizer step is taken and
+the capture finds libraries and workspaces initialised). At most `max_graphs` are kept (LRU).
+Gradients live in persistent tensors that every graph zeroes and accumulates into, so the one
+update graph serves all of them.
+
+Same kernels, same arithmetic as the eager step: a replay is bit-identical to an eager step on
+the same state and batch. With world > 1 the forward contains the contrastive loss's
+all_gather; graph mode is then opt-in (bench --graph-dp), the default keeps the eager path.
 """
+from collections import OrderedDict
+
 import torch
 
 
+def _clone_batch(batch):
+    return {k: v.clone() for k, v in batch.items()}
+
+
+def _detached(T):
+    """Loss dict without autograd history: a live autograd graph keeps the parameters'
+    AccumulateGrad nodes (and the stream they were created on) alive, and a later capture on
+    another stream would then run the gradient accumulation outside the captured graph."""
+    return {k: (v.detach() if torch.is_tensor(v) else v) for k, v in T.items()}
+
+
 class GraphedStep:
-    def __init__(self, inner, example_batch, warmup=3):
+    def __init__(self, inner, example_batch=None, warmup=0, max_graphs=6):
         self.inner = inner
-        # tensors only: a UniqueRows entry (data-dependent shapes) cannot live in static buffers,
-        # so the graphed step encodes every source slot
-        self.static = {k: v.clone() for k, v in example_batch.items() if torch.is_tensor(v)}
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):   # warm-up: library loads, allocator, hipBLASLt workspaces
-            for _ in range(warmup):
-                inner.step(self.static)
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        self.pool = torch.cuda.graph_pool_handle()
-        self.g_fwd_bwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fwd_bwd, pool=self.pool):
-            inner.optimizer.zero_grad(set_to_none=True)
-            loss, self.T = inner.forward(self.static)
-            loss.backward()
-        self.g_update = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_update, pool=self.pool):
-            inner.clip_and_step()
+        self.max_graphs = max_graphs
+        self.graphs = OrderedDict()       # key -> (static batch, graph, loss dict)
+        self.g_update = None
+        self.grads = None
+        if warmup:                         # optional plain eager steps before the first capture
+            main = torch.cuda.current_stream()
+            side = torch.cuda.Stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    inner.step(example_batch)
+            main.wait_stream(side)
 
     @property
     def models(self):
@@ -50,10 +61,63 @@ class GraphedStep:
     def optimizer(self):
         return self.inner.optimizer
 
+    @staticmethod
+    def key(batch):
+        uq = batch.get("src_unique")
+        return None if uq is None else uq.U
+
+    def _eager(self, batch, epoch):
+        if self.grads is None:                       # first step: torch allocates the grads
+            T = self.inner.step(batch, epoch)
+            params = [p for m in self.inner.models.values() for p in m.parameters() if p.grad is not None]
+            self.grads = [p.grad for p in params]
+            return _detached(T)
+        torch._foreach_zero_(self.grads)             # keep the persistent grad tensors
+        loss, T = self.inner.forward(batch, epoch)
+        loss.backward()
+        del loss
+        self.inner.reduce_gradients()
+        self.inner.clip_and_step()
+        return _detached(T)
+
+    def _capture(self, key, batch, epoch):
+        static = _clone_batch(batch)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            torch._foreach_zero_(self.grads)
+            loss, T = self.inner.forward(static, epoch)
+            loss.backward()
+        T = _detached(T)
+        del loss
+        if self.g_update is None:
+            gu = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gu):
+                self.inner.clip_and_step()
+            self.g_update = gu
+        self.graphs[key] = (static, g, T)
+        while len(self.graphs) > self.max_graphs:
+            self.graphs.popitem(last=False)
+
     def step(self, batch, epoch=0):
-        for k, v in self.static.items():
-            v.copy_(batch[k], non_blocking=True)
-        self.g_fwd_bwd.replay()
+        k = self.key(batch)
+        ent = self.graphs.get(k)
+        if ent is None:
+            # the batch's real step runs eagerly on a side stream (that also warms up library
+            # handles / workspaces for the capture stream, as capture requires), then capture
+            main = torch.cuda.current_stream()
+            side = torch.cuda.Stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                T = self._eager(batch, epoch)
+            main.wait_stream(side)
+            self._capture(k, batch, epoch)
+            return T
+        self.graphs.move_to_end(k)
+        static, g, T = ent
+        for name, v in static.items():
+            v.copy_(batch[name], non_blocking=True)
+        g.replay()
         self.inner.reduce_gradients()
         self.g_update.replay()
-        return self.T
+        return T

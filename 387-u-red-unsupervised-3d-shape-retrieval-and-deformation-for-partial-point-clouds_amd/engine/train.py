@@ -209,16 +209,16 @@ class TrainStep:
                 "embedding_layer": m["embedding_layer"].state_dict()}
 
 
-def batch_to_device(b, device, num_sources=None):
+def batch_to_device(b, device, num_sources=None, bucket=None):
     """Host batch -> device tensors. With num_sources (the source DB size) the distinct source
     parts of the batch are also computed here, on the host labels (UniqueRows; used by
-    TrainStep unless cfg["unique_sources"] is False). Left out for HIP-graph replay, whose
-    static buffers need fixed shapes."""
+    TrainStep unless cfg["unique_sources"] is False); `bucket` pads their count for HIP-graph
+    replay (engine/graph.py keeps one graph per padded count)."""
     out = {"x": torch.as_tensor(b["x"]).to(device), "labels": torch.as_tensor(b["labels"]).to(device),
            "tgt_sem": torch.as_tensor(b["tgt_sem"]).to(device),
            "src_labels": torch.as_tensor(b["src_labels"]).to(device)}
     if num_sources is not None:
-        out["src_unique"] = UniqueRows(b["src_labels"], num_sources, device)
+        out["src_unique"] = UniqueRows(b["src_labels"], num_sources, device, bucket=bucket)
     return out
 
 
@@ -237,7 +237,7 @@ class SyntheticLoader:
             b = synthetic.make_batch(self.cfg["batch_size"], self.cfg.get("num_points", 2048), self.ns,
                                      max_parts=self.cfg["MAX_NUM_PARTS"], parts=self.cfg.get("parts", 4),
                                      seed=self.seed * 100003 + i)
-            yield batch_to_device(b, self.device, None if self.cfg.get("cuda_graph") else self.ns)
+            yield batch_to_device(b, self.device, self.ns, bucket=8 if self.cfg.get("cuda_graph") else None)
 
 
 class _ScalarLog:

@@ -119,15 +119,24 @@ class UniqueRows:
     uniq [U] (db row of each distinct part), inverse [R] (distinct part of each slot),
     order [R] (slots sorted by distinct part, stable), off int32 [U+1], w float32 [U] (copies).
     Built on the host from the host-side labels (no device sync), then copied once.
+    bucket: pad U up to a multiple of `bucket` with zero-weight groups (a copy of the last
+    distinct part, empty expand segment): they add nothing to the batch statistics and get
+    zero gradient, and a HIP-graph step then sees a handful of distinct shapes only.
     """
 
-    def __init__(self, labels_host, num_sources, device):
+    def __init__(self, labels_host, num_sources, device, bucket=None):
         import numpy as np
         s = np.asarray(labels_host).reshape(-1).astype(np.int64)
         idx = np.where(s < 0, s + num_sources, s)      # python negative indexing (dataset_utils.py:800-805)
         uniq, inv, cnt = np.unique(idx, return_inverse=True, return_counts=True)
         order = np.argsort(inv, kind="stable")
         off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
+        if bucket:
+            pad = min(-(-uniq.shape[0] // bucket) * bucket, s.shape[0]) - uniq.shape[0]
+            if pad > 0:
+                uniq = np.concatenate([uniq, np.full(pad, uniq[-1])])
+                cnt = np.concatenate([cnt, np.zeros(pad, cnt.dtype)])
+                off = np.concatenate([off, np.full(pad, off[-1], np.int32)])
         self.U = int(uniq.shape[0])
         self.uniq = torch.from_numpy(uniq).to(device)
         self.inverse = torch.from_numpy(inv.reshape(-1).astype(np.int64)).to(device)
@@ -135,5 +144,20 @@ class UniqueRows:
         self.off = torch.from_numpy(off).to(device)
         self.w = torch.from_numpy(cnt.astype(np.float32)).to(device)
 
+    FIELDS = ("uniq", "inverse", "order", "off", "w")
+
     def expand(self, xu):
         return ExpandGroupsFn.apply(xu, self.inverse, self.order, self.off)
+
+    def clone(self):
+        c = UniqueRows.__new__(UniqueRows)
+        c.U = self.U
+        for f in self.FIELDS:
+            setattr(c, f, getattr(self, f).clone())
+        return c
+
+    def copy_(self, other, non_blocking=False):
+        assert other.U == self.U, "UniqueRows.copy_: different distinct-part counts"
+        for f in self.FIELDS:
+            getattr(self, f).copy_(getattr(other, f), non_blocking=non_blocking)
+        return self

@@ -178,6 +178,8 @@ def main():
                     help="replay the step as HIP graphs (engine/graph.py; N=1 unless --graph-dp). Measured "
                          "equal to eager once the step has no host syncs, so eager is the default")
     ap.add_argument("--graph-dp", action="store_true", help="HIP-graph replay also when N > 1")
+    ap.add_argument("--graph-bucket", type=int, default=1,
+                    help="graph mode: pad the distinct-source-part count to a multiple of this (one graph per count)")
     ap.add_argument("--all-slots", action="store_true",
                     help="encode every source slot (no unique-source encoding) in the timed run")
     ap.add_argument("--no-all-slots-rate", action="store_true",
@@ -206,11 +208,12 @@ def main():
     eager = DataParallelStep(cfg, db, dev)
     cfg["unique_sources"] = not args.all_slots
     batches = [batch_to_device(synthetic.make_batch(args.batch, args.points, db.num_sources, parts=args.parts,
-                                                    seed=1000 * rank + i), dev,
-                               None if use_graph else db.num_sources) for i in range(4)]
-    if use_graph:   # capture (after 3 eager warm-up steps on batch 0); replays below
+                                                    seed=1000 * rank + i), dev, db.num_sources,
+                               bucket=args.graph_bucket if use_graph else None) for i in range(4)]
+    if use_graph:   # one graph per padded distinct-part count, captured after that batch's eager step
         from engine.graph import GraphedStep
-        step = GraphedStep(eager, batches[0])
+        step = GraphedStep(eager)
+        args.warmup = max(args.warmup, len(batches))   # every batch's graph is captured before timing
     else:
         step = eager
 
@@ -252,7 +255,7 @@ def main():
         return steps * world / float(tt.item())
 
     all_slots_rate = None
-    if not args.no_all_slots_rate and cfg["unique_sources"] and not use_graph:
+    if not args.no_all_slots_rate and cfg["unique_sources"]:
         cfg["unique_sources"] = False      # every one of the B x 16 source slots encoded
         all_slots_rate = timed_rate(args.steps)
         cfg["unique_sources"] = True
@@ -307,7 +310,7 @@ def main():
                                   for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
     if all_slots_rate is not None:
         extra["all_slots_iters_s"] = round(all_slots_rate, 4)
-    extra["unique_sources"] = bool(cfg["unique_sources"]) and not use_graph
+    extra["unique_sources"] = bool(cfg["unique_sources"])
     extra["chamfer_gpair_s"] = round(chamfer_rate(dev), 1)
     extra["pseudo_label_dcd"] = pair_rate(dev)
     extra["loss"] = loss_val

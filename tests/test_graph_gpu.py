@@ -38,3 +38,53 @@ def test_graph_replay_equals_eager(dev):
     for name in ("src_encoder_all", "param_decoder_full", "re_residual_net_full"):
         for (k, pa), (_, pb) in zip(a.models[name].state_dict().items(), b.models[name].state_dict().items()):
             assert torch.equal(pa, pb), (name, k)
+
+
+def test_graph_replay_unique_sources_equals_eager(dev):
+    """Unique-source batches padded to buckets: one captured graph per padded count (two keys
+    here), replays bitwise-equal to eager steps on the same batches; padding groups (weight 0)
+    change nothing."""
+    from dataset import synthetic
+    from engine.graph import GraphedStep
+    from engine.train import batch_to_device
+    cfg = dict(CFG, cuda_graph=True)
+    parts = [[3, 2], [5, 4], [3, 2], [5, 4], [2, 2]]
+    batches = [batch_to_device(synthetic.make_batch(2, 128, 24, parts=p, seed=70 + i), dev, 24, bucket=4)
+               for i, p in enumerate(parts)]
+    keys = {GraphedStep.key(b) for b in batches}
+    assert len(keys) >= 2 and None not in keys
+    a, b = _make(dev, cfg), _make(dev, cfg)
+    g = GraphedStep(a)
+    for i in range(2):
+        b.step(batches[0])
+        g.step(batches[0])
+    for rnd in range(2):
+        for i, bt in enumerate(batches):
+            la = g.step(bt)["all_loss"].clone()
+            lb = b.step(bt)["all_loss"]
+            assert torch.equal(la, lb), (rnd, i, la.item(), lb.item())
+    assert len(g.graphs) == len(keys)
+    for name in ("src_encoder_all", "recon_decoder_src", "param_decoder_full"):
+        for (k, pa), (_, pb) in zip(a.models[name].state_dict().items(), b.models[name].state_dict().items()):
+            assert torch.equal(pa, pb), (name, k)
+
+
+def test_padded_unique_rows_match_unpadded(dev):
+    """Zero-weight padding groups leave losses and gradients unchanged (up to summation order)."""
+    from dataset import synthetic
+    from engine.train import batch_to_device
+    bt = synthetic.make_batch(2, 128, 24, parts=[3, 2], seed=90)
+    p = batch_to_device(bt, dev, 24, bucket=16)
+    u = batch_to_device(bt, dev, 24)
+    assert p["src_unique"].U > u["src_unique"].U
+    a, b = _make(dev, CFG), _make(dev, CFG)
+    la, Ta = a.forward(p)
+    lb, Tb = b.forward(u)
+    assert abs(la.item() - lb.item()) <= 1e-6 * abs(lb.item())
+    la.backward()
+    lb.backward()
+    for (k, pa), (_, pb) in zip(a.models["src_encoder_all"].named_parameters(),
+                                b.models["src_encoder_all"].named_parameters()):
+        if pa.grad is None:
+            continue
+        assert (pa.grad - pb.grad).norm() <= 1e-4 * pb.grad.norm() + 1e-6, k
