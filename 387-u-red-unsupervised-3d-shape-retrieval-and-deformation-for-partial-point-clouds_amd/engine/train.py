@@ -114,6 +114,30 @@ class TrainStep:
         self.db = db
         self.models, self.optimizer, self.scheduler = get_models(cfg, device)
         self.np_per_part = db.points.shape[1]
+        dev = torch.device(device or cfg["device"])
+        self.side_stream = (torch.cuda.Stream(device=dev)
+                            if dev.type == "cuda" and cfg.get("stream_overlap", False) else None)
+
+    def _source_branch(self, uq, src_points, src_sem_f, B, P):
+        """src_encoder_all + recon_decoder_src (engine/train.py:210-216) -> codes [B*P, C],
+        recon_src_p [B, P, NP, 3]."""
+        M = self.models
+        if uq is not None:
+            # unique source encoding: the slots' inputs are functions of their source part
+            # only, so the encoder and recon_decoder_src run once per distinct part with row
+            # multiplicities (BN statistics / backward of the full batch), then expand
+            rw = RowWeights(uq.w, self.np_per_part)
+            with torch.no_grad():
+                sem_u = M["embedding_layer"](self.db.sem[uq.uniq])
+            code_u, pp_u = M["src_encoder_all"].forward_pointmajor(self.db.points[uq.uniq].unsqueeze(0),
+                                                                   sem_u.unsqueeze(0), rw=rw)
+            rec_u = M["recon_decoder_src"].forward_split(pp_u, code_u, code_first=True,
+                                                         group_rows=self.np_per_part, rw=rw)
+            return uq.expand(code_u), uq.expand(rec_u.view(uq.U, -1)).view(B, P, -1, 3)
+        codes, src_pp = M["src_encoder_all"].forward_pointmajor(src_points, src_sem_f)
+        recon_src_p = M["recon_decoder_src"].forward_split(src_pp, codes, code_first=True,
+                                                           group_rows=self.np_per_part).view(B, P, -1, 3)
+        return codes, recon_src_p
 
     def forward(self, batch, epoch=0):
         cfg, M = self.cfg, self.models
@@ -128,28 +152,28 @@ class TrainStep:
             tgt_sem_f = emb(batch["tgt_sem"])
         src_points = get_source_points(src_labels, self.db)
         uq = batch.get("src_unique") if cfg.get("unique_sources", True) else None
-        if uq is not None:
-            # unique source encoding: the slots' inputs are functions of their source part
-            # only, so the encoder and recon_decoder_src run once per distinct part with row
-            # multiplicities (BN statistics / backward of the full batch), then expand
-            rw = RowWeights(uq.w, self.np_per_part)
-            with torch.no_grad():
-                sem_u = emb(self.db.sem[uq.uniq])
-            code_u, pp_u = M["src_encoder_all"].forward_pointmajor(self.db.points[uq.uniq].unsqueeze(0),
-                                                                   sem_u.unsqueeze(0), rw=rw)
-            rec_u = M["recon_decoder_src"].forward_split(pp_u, code_u, code_first=True,
-                                                         group_rows=self.np_per_part, rw=rw)
-            codes = uq.expand(code_u)
-            recon_src_p = uq.expand(rec_u.view(uq.U, -1)).view(B, P, -1, 3)
+        side = self.side_stream
+        if side is not None:
+            # the source branch (encoder + recon_decoder_src, forward and — autograd runs each
+            # node on its forward stream — backward) overlaps the target branch: each fills the
+            # other's GEMM tails and small-kernel gaps
+            main = torch.cuda.current_stream(x.device)
+            side.wait_stream(main)
+            src_points.record_stream(side)      # main-stream tensors read by the side stream
+            src_sem_f.record_stream(side)
+            with torch.cuda.stream(side):
+                codes, recon_src_p = self._source_branch(uq, src_points, src_sem_f, B, P)
         else:
-            codes, src_pp = M["src_encoder_all"].forward_pointmajor(src_points, src_sem_f)
-            recon_src_p = M["recon_decoder_src"].forward_split(src_pp, codes, code_first=True,
-                                                               group_rows=self.np_per_part).view(B, P, -1, 3)
+            codes, recon_src_p = self._source_branch(uq, src_points, src_sem_f, B, P)
         tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
         target_part_f, _, re_in, mask_part, part_x, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
         recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
         re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
                                                          off=re_in.off).view(B, N, 3)
+        if side is not None:
+            main.wait_stream(side)
+            codes.record_stream(main)
+            recon_src_p.record_stream(main)
         codes = codes.view(B, P, -1)
         params_full = M["param_decoder_full"](tcode, codes, None)
         out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)

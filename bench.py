@@ -180,6 +180,8 @@ def main():
     ap.add_argument("--graph-dp", action="store_true", help="HIP-graph replay also when N > 1")
     ap.add_argument("--graph-bucket", type=int, default=1,
                     help="graph mode: pad the distinct-source-part count to a multiple of this (one graph per count)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="run the source branch on a second stream (measured neutral: the GEMMs fill the GPU)")
     ap.add_argument("--all-slots", action="store_true",
                     help="encode every source slot (no unique-source encoding) in the timed run")
     ap.add_argument("--no-all-slots-rate", action="store_true",
@@ -204,6 +206,7 @@ def main():
     cfg = workload_cfg(args)
     use_graph = args.graph and (world == 1 or args.graph_dp)
     cfg["cuda_graph"] = use_graph
+    cfg["stream_overlap"] = args.overlap
     db, _ = load_sources(cfg, dev)
     eager = DataParallelStep(cfg, db, dev)
     cfg["unique_sources"] = not args.all_slots
