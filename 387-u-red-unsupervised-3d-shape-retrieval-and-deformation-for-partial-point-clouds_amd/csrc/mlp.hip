@@ -506,11 +506,15 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                         const size_t ge = (size_t)(row / d.pool_group_rows) * d.N + col;
                         if (d.pool_idx[ge] == row) dh += d.pool_grad[ge];
                     }
+                    if (d.gadd && ok) dh += d.gadd[(size_t)row * d.ldg + col];
                     const float y = yh[i][r];
                     float g, xh;
-                    if (d.bwd_res) {
+                    if (d.bwd_res == URED_ACT_RES) {
                         g = dh;
                         xh = (fmaxf(y, 0.f) - mu) * is;
+                    } else if (d.bwd_res == URED_ACT_BN) {
+                        g = dh;
+                        xh = (y - mu) * is;
                     } else {
                         g = (__builtin_fmaf(y, sc, sh) > 0.f) ? dh : 0.f;
                         xh = (y - mu) * is;
@@ -1135,13 +1139,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
 }
 
 __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restrict__ ws, int M, int N, int group_rows,
-        const float* __restrict__ scale, const float* __restrict__ shift, float* pooled, int* argidx) {
+        const float* __restrict__ scale, const float* __restrict__ shift, int relu, float* pooled, int* argidx) {
     const int n = blockIdx.x * 256 + threadIdx.x;
     const int g = blockIdx.y;
     if (n >= N) return;
     const int bpg = group_rows / BM;
     const float sc = scale[n], sh = shift[n];
-    const bool up = sc >= 0.f;    // relu(sc*y+sh) is non-decreasing in y iff sc >= 0
+    const bool up = sc >= 0.f;    // (relu of) sc*y+sh is non-decreasing in y iff sc >= 0
     float best = up ? -__builtin_inff() : __builtin_inff();
     int bi = 0x7fffffff;
     for (int b = g * bpg; b < (g + 1) * bpg && b * BM < M; ++b) {
@@ -1150,13 +1154,14 @@ __global__ __launch_bounds__(256) void pool_finalize_kernel(const float* __restr
         const int vi = reinterpret_cast<const int*>(pw)[(up ? 1 : 3) * N + n];
         if ((up ? v > best : v < best) || (v == best && vi < bi)) { best = v; bi = vi; }
     }
-    pooled[(size_t)g * N + n] = fmaxf(__builtin_fmaf(best, sc, sh), 0.f);
+    const float pv = __builtin_fmaf(best, sc, sh);
+    pooled[(size_t)g * N + n] = relu ? fmaxf(pv, 0.f) : pv;
     argidx[(size_t)g * N + n] = bi;
 }
 
 // general max-pool (any group size): per (group, column) scan of the raw layer output
 __global__ __launch_bounds__(256) void pool_rows_kernel(const float* __restrict__ Y, int N, int group_rows,
-        const float* __restrict__ scale, const float* __restrict__ shift, float* pooled, int* argidx) {
+        const float* __restrict__ scale, const float* __restrict__ shift, int relu, float* pooled, int* argidx) {
     const int n = blockIdx.x * 256 + threadIdx.x;
     const int g = blockIdx.y;
     if (n >= N) return;
@@ -1168,8 +1173,36 @@ __global__ __launch_bounds__(256) void pool_rows_kernel(const float* __restrict_
         const float v = Y[(size_t)r * N + n];
         if (up ? v > best : v < best) { best = v; bi = r; }
     }
-    pooled[(size_t)g * N + n] = fmaxf(__builtin_fmaf(best, sc, sh), 0.f);
+    const float pv = __builtin_fmaf(best, sc, sh);
+    pooled[(size_t)g * N + n] = relu ? fmaxf(pv, 0.f) : pv;
     argidx[(size_t)g * N + n] = bi;
+}
+
+// out[m][n] = act(Y[m][n]*scale[n] + shift[n]) (act = relu or identity): the BatchNorm
+// (+ReLU) output materialised, where a caller needs the activation itself (PointNet's
+// pointfeat / feature-transform input); float4 along n when N % 4 == 0.
+__global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ Y, int M, int N, int ldy,
+        const float* __restrict__ scale, const float* __restrict__ shift, int relu, float* __restrict__ out, int ldo,
+        int vec) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (vec) {
+        const int n4 = N >> 2;
+        if (i >= (long long)M * n4) return;
+        const int m = (int)(i / n4), n = (int)(i % n4) * 4;
+        const float4 y = *reinterpret_cast<const float4*>(Y + (size_t)m * ldy + n);
+        const float4 s = *reinterpret_cast<const float4*>(scale + n);
+        const float4 t = *reinterpret_cast<const float4*>(shift + n);
+        float4 o;
+        o.x = __builtin_fmaf(y.x, s.x, t.x); o.y = __builtin_fmaf(y.y, s.y, t.y);
+        o.z = __builtin_fmaf(y.z, s.z, t.z); o.w = __builtin_fmaf(y.w, s.w, t.w);
+        if (relu) { o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f); }
+        *reinterpret_cast<float4*>(out + (size_t)m * ldo + n) = o;
+    } else {
+        if (i >= (long long)M * N) return;
+        const int m = (int)(i / N), n = (int)(i % N);
+        const float v = __builtin_fmaf(Y[(size_t)m * ldy + n], scale[n], shift[n]);
+        out[(size_t)m * ldo + n] = relu ? fmaxf(v, 0.f) : v;
+    }
 }
 
 // out[g][n] = sum of rows [r0, r1) of column n. Block = 4 waves x 64 columns; wave w sums
@@ -1394,26 +1427,41 @@ int ured_bn_bwd_apply(const float* G, const float* Y, int M, int N, int ld, int 
 }
 
 int ured_pool_finalize(const float* pool_ws, int M, int N, int group_rows, const float* scale,
-                       const float* shift, float* pooled, int* argidx, void* stream) {
+                       const float* shift, int relu, float* pooled, int* argidx, void* stream) {
     ured::clear_error();
     URED_REQUIRE(M > 0 && N > 0 && group_rows > 0 && group_rows % BM == 0 && M % group_rows == 0,
                  "ured_pool_finalize: M=%d must be a multiple of group_rows=%d (multiple of %d)", M, group_rows, BM);
     URED_REQUIRE(pool_ws && scale && shift && pooled && argidx, "ured_pool_finalize: null pointer");
     dim3 grid((N + 255) / 256, M / group_rows);
     hipLaunchKernelGGL(pool_finalize_kernel, grid, dim3(256), 0, (hipStream_t)stream, pool_ws, M, N, group_rows,
-                       scale, shift, pooled, argidx);
+                       scale, shift, relu, pooled, argidx);
     return ured::launch_status("ured_pool_finalize");
 }
 
 int ured_pool_rows(const float* Y, int M, int N, int group_rows, const float* scale, const float* shift,
-                   float* pooled, int* argidx, void* stream) {
+                   int relu, float* pooled, int* argidx, void* stream) {
     ured::clear_error();
     URED_REQUIRE(M > 0 && N > 0 && group_rows > 0 && M % group_rows == 0, "ured_pool_rows: bad sizes M=%d group_rows=%d", M, group_rows);
     URED_REQUIRE(M / group_rows <= 65535, "ured_pool_rows: too many groups");
     URED_REQUIRE(Y && scale && shift && pooled && argidx, "ured_pool_rows: null pointer");
     dim3 grid((N + 255) / 256, M / group_rows);
-    hipLaunchKernelGGL(pool_rows_kernel, grid, dim3(256), 0, (hipStream_t)stream, Y, N, group_rows, scale, shift, pooled, argidx);
+    hipLaunchKernelGGL(pool_rows_kernel, grid, dim3(256), 0, (hipStream_t)stream, Y, N, group_rows, scale, shift, relu, pooled, argidx);
     return ured::launch_status("ured_pool_rows");
+}
+
+int ured_bn_act(const float* Y, int M, int N, int ldy, const float* scale, const float* shift, int relu,
+                float* out, int ldo, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(M >= 0 && N >= 0 && ldy >= N && ldo >= N, "ured_bn_act: bad sizes M=%d N=%d ldy=%d ldo=%d", M, N, ldy, ldo);
+    if (M == 0 || N == 0) return 0;
+    URED_REQUIRE(Y && scale && shift && out, "ured_bn_act: null pointer");
+    const int v4 = (N & 3) == 0 && (ldy & 3) == 0 && (ldo & 3) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(Y) | reinterpret_cast<uintptr_t>(out) |
+                     reinterpret_cast<uintptr_t>(scale) | reinterpret_cast<uintptr_t>(shift)) & 15) == 0;
+    const long long items = (long long)M * (v4 ? N / 4 : N);
+    hipLaunchKernelGGL(bn_act_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       Y, M, N, ldy, scale, shift, relu, out, ldo, v4);
+    return ured::launch_status("ured_bn_act");
 }
 
 int ured_group_colsum(const float* X, int ldx, int N, const int* off, int group_rows, int G,

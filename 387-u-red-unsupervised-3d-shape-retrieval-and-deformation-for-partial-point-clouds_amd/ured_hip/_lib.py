@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libured_hip.so"
 LIB_PATH = os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

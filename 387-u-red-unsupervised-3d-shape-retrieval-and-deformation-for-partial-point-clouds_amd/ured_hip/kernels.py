@@ -11,6 +11,7 @@ from . import _lib
 
 PRO_NONE, PRO_ENC, PRO_RES = 0, 1, 2
 EPI_STORE, EPI_FWD, EPI_BNBWD, EPI_SPLITK = 0, 1, 2, 3
+ACT_ENC, ACT_RES, ACT_BN = 0, 1, 2      # EPI_BNBWD: Conv->BN->ReLU, Conv->ReLU->BN, Conv->BN
 BM = 128
 
 _P, _I = ctypes.c_void_p, ctypes.c_int
@@ -25,7 +26,7 @@ class GemmDesc(ctypes.Structure):
                 ("gidx", _P), ("group_rows", _I), ("stat_relu", _I), ("stat_ws", _P), ("pool_ws", _P),
                 ("Yp", _P), ("ldy", _I), ("bn_mean", _P), ("bn_invstd", _P), ("bn_scale", _P), ("bn_shift", _P),
                 ("bwd_res", _I), ("pool_idx", _P), ("pool_grad", _P), ("pool_group_rows", _I),
-                ("bwd_ws", _P), ("splits", _I)]
+                ("bwd_ws", _P), ("splits", _I), ("gadd", _P), ("ldg", _I)]
 
 
 _SIGS = {
@@ -34,10 +35,11 @@ _SIGS = {
     "ured_bn_fwd_finalize": [_P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "ured_bn_bwd_finalize": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P],
     "ured_bn_bwd_apply": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
-    "ured_pool_finalize": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
+    "ured_pool_finalize": [_P, _I, _I, _I, _P, _P, _I, _P, _P, _P],
     "ured_group_colsum": [_P, _I, _I, _P, _I, _I, _P, _I, _P],
     "ured_group_colsum_split": [_P, _I, _I, _P, _I, _I, _I, _P, _P, _I, _P],
-    "ured_pool_rows": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
+    "ured_pool_rows": [_P, _I, _I, _I, _P, _P, _I, _P, _P, _P],
+    "ured_bn_act": [_P, _I, _I, _I, _P, _P, _I, _P, _I, _P],
 }
 _lib.register(_SIGS)
 
@@ -58,7 +60,7 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro
          epi=EPI_STORE, A_off=0, B_off=0, C_off=0, A2=None, lda2=0, k1=None, pro_s=None, pro_t=None, bias=None,
          rowbias=None, ldr=0, gidx=None, group_rows=0, stat_relu=False, stat_ws=None, pool_ws=None,
          Yp=None, ldy=0, bn=None, bwd_res=False, pool_idx=None, pool_grad=None, pool_group_rows=0,
-         bwd_ws=None, splits=1):
+         bwd_ws=None, splits=1, gadd=None, ldg=0):
     """One ured_gemm launch. Offsets are in elements of the respective tensor."""
     d = GemmDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
@@ -74,9 +76,10 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro
     d.Yp, d.ldy = _p(Yp), int(ldy)
     if bn is not None:
         d.bn_mean, d.bn_invstd, d.bn_scale, d.bn_shift = _p(bn.mean), _p(bn.invstd), _p(bn.scale), _p(bn.shift)
-    d.bwd_res = int(bool(bwd_res))
+    d.bwd_res = int(bwd_res)     # ACT_ENC (False) / ACT_RES (True) / ACT_BN
     d.pool_idx, d.pool_grad, d.pool_group_rows = _p(pool_idx), _p(pool_grad), int(pool_group_rows)
     d.bwd_ws, d.splits = _p(bwd_ws), int(splits)
+    d.gadd, d.ldg = _p(gadd), int(ldg)
     _lib.call("ured_gemm", ctypes.byref(d), _lib.stream_of(C))
 
 
@@ -137,23 +140,32 @@ def bn_bwd_apply(G, Y, res, mean, coefs, want_colsum=True, rw=None):
     return dY, cs
 
 
-def pool_finalize(pool_ws, M, N, group_rows, scale, shift):
+def pool_finalize(pool_ws, M, N, group_rows, scale, shift, relu=True):
     G = M // group_rows
     pooled = torch.empty(G, N, device=pool_ws.device)
     argidx = torch.empty(G, N, device=pool_ws.device, dtype=torch.int32)
-    _lib.call("ured_pool_finalize", _p(pool_ws), int(M), int(N), int(group_rows), _p(scale), _p(shift),
+    _lib.call("ured_pool_finalize", _p(pool_ws), int(M), int(N), int(group_rows), _p(scale), _p(shift), int(relu),
               _p(pooled), _p(argidx), _lib.stream_of(pool_ws))
     return pooled, argidx
 
 
-def pool_rows(Y, group_rows, scale, shift):
+def pool_rows(Y, group_rows, scale, shift, relu=True):
     M, N = Y.shape
     G = M // group_rows
     pooled = torch.empty(G, N, device=Y.device)
     argidx = torch.empty(G, N, device=Y.device, dtype=torch.int32)
-    _lib.call("ured_pool_rows", _p(Y), int(M), int(N), int(group_rows), _p(scale), _p(shift), _p(pooled),
+    _lib.call("ured_pool_rows", _p(Y), int(M), int(N), int(group_rows), _p(scale), _p(shift), int(relu), _p(pooled),
               _p(argidx), _lib.stream_of(Y))
     return pooled, argidx
+
+
+def bn_act(Y, st, relu=True):
+    """act(Y * st.scale + st.shift) materialised ([M][N])."""
+    M, N = Y.shape
+    out = torch.empty(M, N, device=Y.device)
+    _lib.call("ured_bn_act", _p(Y), int(M), int(N), int(Y.stride(0)), _p(st.scale), _p(st.shift), int(relu),
+              _p(out), int(N), _lib.stream_of(Y))
+    return out
 
 
 def group_colsum(X, N, G, *, off=None, group_rows=0, ldx=None, out=None, rows=None):

@@ -16,6 +16,7 @@ per-call index bookkeeping is Python.
 import torch
 from torch.autograd import Function
 
+from . import _lib
 from . import kernels as K
 
 BN_EPS = 1e-5
@@ -310,3 +311,144 @@ class ResidualNetFn(Function):
         if Cc > 0:
             K.gemm(G, Cc, N1, D, N1, W1, ld1, dcode, Cc, b_kmajor=True, B_off=code_off)
         return (None, dpp, dcode) + tuple(grads)
+
+
+class ChainSpec:
+    """Static description of one PointChainFn call (a PointNet conv chain).
+
+    acts: per layer K.ACT_ENC (Conv->BN->ReLU) or K.ACT_BN (Conv->BN; last layer only)
+    group_rows: points per cloud (the max-pool groups)
+    pool: max-pool the last layer's activation over each group -> pooled [G, N_L]
+    want_act: also return the last layer's activation materialised [M, N_L]
+    bn_modules: the BatchNorm1d modules (running stats updated in place when training)
+    """
+
+    def __init__(self, acts, group_rows, training, bn_modules, pool=True, want_act=False):
+        assert all(a == K.ACT_ENC for a in acts[:-1]), "inner layers feed a GEMM prologue: Conv->BN->ReLU only"
+        self.acts, self.group_rows, self.training = list(acts), int(group_rows), training
+        self.bn_modules, self.pool, self.want_act = bn_modules, pool, want_act
+
+
+class PointChainFn(Function):
+    """Conv1d(k=1)+BatchNorm1d(+ReLU) x L on point-major x [M, Cin], then max-pool over groups of
+    spec.group_rows points and/or the last activation (PointNet STN3d / STNkd / PointNetEncoder
+    conv stacks, network/pointnet/pointnet_utils.py:27-33,62-68,109-127).
+
+    params: W1,b1,g1,be1, ..., WL,bL,gL,beL. Returns (pooled [G, N_L], act [M, N_L]); an output
+    not asked for is an empty tensor. Backward: the last layer's gradient (scattered pool
+    gradient + act gradient) enters through a K = 0 BN-backward epilogue; every layer below is
+    the fused dgrad + BN-backward GEMM of PointEncoderFn; dx = dY1 @ W1.
+    """
+
+    @staticmethod
+    def forward(ctx, spec, x, *params):
+        _lib.require_device(x, *params)
+        x = x.contiguous()
+        M = x.shape[0]
+        GR = spec.group_rows
+        L = len(spec.acts)
+        dev = x.device
+        Ys, states = [], []
+        h, pro, st = x, K.PRO_NONE, None
+        pool_ws = None
+        for i in range(L):
+            W = params[4 * i].reshape(params[4 * i].shape[0], -1)
+            N = W.shape[0]
+            Y = torch.empty(M, N, device=dev)
+            sws = torch.empty(K.nblocks(M), 2, N, device=dev)
+            kw = {}
+            if i == L - 1 and spec.pool and GR % K.BM == 0:
+                pool_ws = torch.empty(K.nblocks(M), 4, N, device=dev)
+                kw.update(pool_ws=pool_ws, group_rows=GR)
+            K.gemm(M, N, W.shape[1], h, h.shape[1], W, W.shape[1], Y, N, pro_a=pro,
+                   pro_s=None if st is None else st.scale, pro_t=None if st is None else st.shift,
+                   bias=params[4 * i + 1], epi=K.EPI_FWD, stat_ws=sws, **kw)
+            spec_i = _LayerBN(spec, i)
+            st = _bn_state(spec_i, 0, sws, M, N, params[4 * i + 2], params[4 * i + 3])
+            Ys.append(Y)
+            states.append(st)
+            h, pro = Y, K.PRO_ENC
+        relu_last = spec.acts[-1] == K.ACT_ENC
+        NL = Ys[-1].shape[1]
+        pooled = argidx = None
+        if spec.pool:
+            if pool_ws is not None:
+                pooled, argidx = K.pool_finalize(pool_ws, M, NL, GR, st.scale, st.shift, relu=relu_last)
+            else:
+                pooled, argidx = K.pool_rows(Ys[-1], GR, st.scale, st.shift, relu=relu_last)
+        act = K.bn_act(Ys[-1], st, relu=relu_last) if spec.want_act else None
+        ctx.spec, ctx.states = spec, states
+        ctx.save_for_backward(x, argidx, *Ys, *params)
+        empty = x.new_empty(0)
+        out_p = pooled if pooled is not None else empty
+        out_a = act if act is not None else x.new_empty(0)
+        if pooled is None:
+            ctx.mark_non_differentiable(out_p)
+        if act is None:
+            ctx.mark_non_differentiable(out_a)
+        return out_p, out_a
+
+    @staticmethod
+    def backward(ctx, dpooled, dact):
+        spec, states = ctx.spec, ctx.states
+        saved = ctx.saved_tensors
+        L = len(spec.acts)
+        x, argidx = saved[0], saved[1]
+        Ys = list(saved[2:2 + L])
+        params = saved[2 + L:]
+        M, Cin = x.shape
+        GR = spec.group_rows
+        dev = x.device
+        grads = [None] * (4 * L)
+        use_pool = spec.pool and dpooled is not None and dpooled.numel() > 0
+        use_act = spec.want_act and dact is not None and dact.numel() > 0
+        dY, Wn = None, None
+        for i in range(L - 1, -1, -1):
+            Y, st = Ys[i], states[i]
+            N = Y.shape[1]
+            G_ = torch.empty(M, N, device=dev)
+            bws = torch.empty(K.nblocks(M), 2, N, device=dev)
+            if i == L - 1:
+                # no GEMM feeds the last layer: K = 0, the epilogue adds the pooled gradient at
+                # the winning rows and the activation's own gradient, masks, and reduces
+                kw = {}
+                if use_pool:
+                    kw.update(pool_idx=argidx, pool_grad=dpooled.contiguous(), pool_group_rows=GR)
+                if use_act:
+                    dact = dact.contiguous()
+                    kw.update(gadd=dact, ldg=N)
+                K.gemm(M, N, 0, Y, N, Y, N, G_, N, b_kmajor=True, epi=K.EPI_BNBWD, Yp=Y, ldy=N, bn=st,
+                       bwd_res=spec.acts[i], bwd_ws=bws, **kw)
+            else:
+                Cn = dY.shape[1]
+                K.gemm(M, N, Cn, dY, Cn, Wn, Wn.shape[1], G_, N, b_kmajor=True, epi=K.EPI_BNBWD,
+                       Yp=Y, ldy=N, bn=st, bwd_res=spec.acts[i], bwd_ws=bws)
+            gamma = params[4 * i + 2]
+            dgamma, dbeta = torch.empty(N, device=dev), torch.empty(N, device=dev)
+            coefs = K.bn_bwd_finalize(bws, M, N, gamma, st.invstd, dgamma, dbeta)
+            dYi, cs = K.bn_bwd_apply(G_, Y, False, st.mean, coefs)
+            W = params[4 * i].reshape(params[4 * i].shape[0], -1)
+            dW = torch.empty(W.shape, device=dev)
+            if i == 0:
+                K.wgrad(dYi, N, x, Cin, N, Cin, M, dW, Cin)
+            else:
+                Xp, stp = Ys[i - 1], states[i - 1]
+                kin = Xp.shape[1]
+                K.wgrad(dYi, N, Xp, kin, N, kin, M, dW, kin, pro=K.PRO_ENC, pro_s=stp.scale, pro_t=stp.shift)
+            grads[4 * i] = dW.view(params[4 * i].shape)
+            grads[4 * i + 1] = K.colsum(cs)
+            grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
+            dY, Wn = dYi, W
+        dx = None
+        if ctx.needs_input_grad[1]:
+            dx = torch.empty(M, Cin, device=dev)
+            K.gemm(M, Cin, dY.shape[1], dY, dY.shape[1], Wn, Wn.shape[1], dx, Cin, b_kmajor=True)
+        return (None, dx) + tuple(grads)
+
+
+class _LayerBN:
+    """Adapter: the BN bookkeeping of layer i of a ChainSpec in _bn_state's form."""
+    __slots__ = ("bn_modules", "training", "eps", "rw")
+
+    def __init__(self, spec, i):
+        self.bn_modules, self.training, self.eps, self.rw = [spec.bn_modules[i]], spec.training, BN_EPS, None

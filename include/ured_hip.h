@@ -34,7 +34,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 1
+#define URED_ABI_VERSION 2
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
@@ -109,9 +109,10 @@ int ured_dcd(const float* dist1, const int* idx1, const float* dist2, const int*
  *               column partials {mean, M2} of p (p = Y, or relu(Y) if stat_relu) into
  *               stat_ws[blk][2][N]; if pool_ws: per block column {max,argmax,min,argmin}
  *               of Y into pool_ws[blk][4][N] (group_rows multiple of 128)
- *   EPI_BNBWD : dh = acc (+ pool_grad[g][n] where pool_idx[g][n] == m); with the previous
- *               layer's (Y, mean, invstd, scale, shift): ENC g = dh*(Y*scale+shift > 0),
- *               xhat = (Y-mean)*invstd; RES g = dh, xhat = (relu(Y)-mean)*invstd;
+ *   EPI_BNBWD : dh = acc (+ pool_grad[g][n] where pool_idx[g][n] == m) (+ gadd[m][n]); with
+ *               the previous layer's (Y, mean, invstd, scale, shift): ENC g = dh*(Y*scale+shift > 0),
+ *               xhat = (Y-mean)*invstd; RES g = dh, xhat = (relu(Y)-mean)*invstd; BN g = dh,
+ *               xhat = (Y-mean)*invstd. K = 0 is allowed (acc = 0: a pooled / extra gradient only);
  *               stores g to C and block column partials {sum g, sum g*xhat} to bwd_ws
  *   EPI_SPLITK: partial sums of the k-range of blockIdx.z stored to C + z*M*ldc
  */
@@ -122,6 +123,10 @@ int ured_dcd(const float* dist1, const int* idx1, const float* dist2, const int*
 #define URED_EPI_FWD 1
 #define URED_EPI_BNBWD 2
 #define URED_EPI_SPLITK 3
+/* EPI_BNBWD activation order of the layer whose output is being differentiated (bwd_res field) */
+#define URED_ACT_ENC 0   /* Conv -> BN -> ReLU */
+#define URED_ACT_RES 1   /* Conv -> ReLU -> BN */
+#define URED_ACT_BN 2    /* Conv -> BN (no activation; PointNet's conv3, pointnet_utils.py:126) */
 
 typedef struct UredGemmDesc {
     int M, N, K;
@@ -139,10 +144,11 @@ typedef struct UredGemmDesc {
     float* pool_ws;                             /* [ceil(M/128)][4][N] or NULL */
     const float* Yp; int ldy;                   /* EPI_BNBWD: previous layer's raw output */
     const float* bn_mean; const float* bn_invstd; const float* bn_scale; const float* bn_shift;
-    int bwd_res;
+    int bwd_res;                                /* URED_ACT_ENC / URED_ACT_RES / URED_ACT_BN */
     const int* pool_idx; const float* pool_grad; int pool_group_rows;
     float* bwd_ws;                              /* [ceil(M/128)][2][N] */
     int splits;                                 /* EPI_SPLITK: gridDim.z (k-range per split = ceil(K/splits/32)*32) */
+    const float* gadd; int ldg;                 /* EPI_BNBWD: optional extra gradient, dh += gadd[m*ldg+n] */
 } UredGemmDesc;
 
 int ured_gemm(const UredGemmDesc* d, void* stream);
@@ -180,13 +186,20 @@ int ured_bn_bwd_apply(const float* G, const float* Y, int M, int N, int ld, int 
                       float* dY, float* colsum_ws, const float* group_w, int group_rows, void* stream);
 
 /* Max-pool finalize (TargetEncoder max_pool1d over each group of group_rows points of
- * relu(scale*Y+shift)): pooled[g][n] and the winning row index argidx[g][n]. */
+ * relu(scale*Y+shift), simple_encoder.py:105; relu = 0: of scale*Y+shift, PointNet's
+ * torch.max over bn3(conv3(x)), pointnet_utils.py:126-127): pooled[g][n] and the winning
+ * row index argidx[g][n] (lowest row on ties). */
 int ured_pool_finalize(const float* pool_ws, int M, int N, int group_rows, const float* scale,
-                       const float* shift, float* pooled, int* argidx, void* stream);
+                       const float* shift, int relu, float* pooled, int* argidx, void* stream);
 
 /* Same result as EPI_FWD pooling + ured_pool_finalize for any group size (a direct scan of Y [M][N]). */
 int ured_pool_rows(const float* Y, int M, int N, int group_rows, const float* scale, const float* shift,
-                   float* pooled, int* argidx, void* stream);
+                   int relu, float* pooled, int* argidx, void* stream);
+
+/* out[m][n] = act(Y[m*ldy+n]*scale[n] + shift[n]), act = relu (relu != 0) or identity: a
+ * BatchNorm(+ReLU) output materialised (PointNet pointfeat, pointnet_utils.py:120,124). */
+int ured_bn_act(const float* Y, int M, int N, int ldy, const float* scale, const float* shift, int relu,
+                float* out, int ldo, void* stream);
 
 /* out[g][n] = sum_{m in [off[g], off[g+1])} X[m*ldx+n] (rows ascending); off == NULL means
  * fixed groups of group_rows rows. G groups. */
