@@ -654,6 +654,9 @@ constexpr int PRO_LDS = 1024;            // max prologue channels staged in LDS 
 // SGPR spills (every epilogue argument stays live across the main loop), so it is compiled
 // out; kept for experiments.
 constexpr bool GEMM_PERSIST = false;
+#ifndef URED_PRO_PACKED
+#define URED_PRO_PACKED 0
+#endif
 constexpr int BUF_DWORD3 = 0x00020000;   // raw buffer, gfx9 family (gfx950)
 
 __host__ __device__ inline bool buf_ok(const UredGemmDesc& d) {
@@ -704,21 +707,37 @@ __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld,
 // track it, so it adds no vmcnt(0) of its own in front of later ds_reads of the stages (it
 // cannot tell the two stages apart, nor count the epilogue's stores behind the prefetch).
 // Completion is ordered explicitly by the K-loop's vmcnt wait before its barrier. Ops the
-// pass cannot see only make its own vmcnt(N) waits conservative (in-order counter). m0 is
-// saved and restored around the instruction.
-__device__ __forceinline__ void dma_lds16(const i32x4& rsrc, unsigned voff, float* lds_dst) {
-    const unsigned lds = __builtin_amdgcn_readfirstlane(
-        (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)lds_dst);
+// pass cannot see only make its own vmcnt(N) waits conservative (in-order counter).
+// One asm block issues a wave's four 1-KB chunks of an operand image: m0 (the LDS
+// destination) is set once from a wave-uniform SGPR byte address and advanced by 1 KB with
+// scalar adds — no per-DMA readfirstlane / generic->LDS pointer conversion — and restored.
+// An s_nop follows each m0 write (SALU m0 write -> LDS-DMA hazard).
+__device__ __forceinline__ void dma4(const i32x4& rsrc, unsigned v0, unsigned v1, unsigned v2, unsigned v3,
+                                     unsigned lds) {
     unsigned saved;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
-                 : "=&s"(saved) : "s"(lds), "v"(voff), "s"(rsrc) : "memory");
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %6, 0 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %3, %6, 0 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %4, %6, 0 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x400\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %5, %6, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(saved) : "s"(lds), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(rsrc) : "memory", "scc");
 }
 
+// lds: wave-uniform LDS byte address of this wave's first chunk of the operand image
 template <bool KM>
-__device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, float* S, int w) {
+__device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, unsigned lds) {
     const unsigned toff = KM ? (unsigned)k0 * (unsigned)ld * 4u : (unsigned)k0 * 4u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dma_lds16(o.rsrc, o.vo[i] + toff, S + (w * 4 + i) * 256);
+    dma4(o.rsrc, o.vo[0] + toff, o.vo[1] + toff, o.vo[2] + toff, o.vo[3] + toff, lds);
 }
 
 template <int PRO>
@@ -776,12 +795,15 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         if (!A_KM && has_a2) buf_setup<false>(ba2, d.A2, d.lda2, d.M, m0_, d.K - d.k1, w, lane);
         buf_setup<B_KM>(bb, d.B, d.ldb, d.N, n0_, kend, w, lane);
     };
+    // this wave's chunk base in the LDS images, as a wave-uniform byte address (SGPR)
+    const unsigned lds_w = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem + (unsigned)w * 4096u);
     auto issue = [&](int stage, int k0, int m0_, int n0_) {
-        float* As = smem + stage * 2 * TILE;
-        float* Bs = As + TILE;
-        if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false>(ba2, d.lda2, k0 - d.k1, As, w);
-        else buf_tile<A_KM>(ba, d.lda, k0, As, w);
-        buf_tile<B_KM>(bb, d.ldb, k0, Bs, w);
+        const unsigned la = lds_w + (unsigned)stage * (2u * TILE * 4u);
+        const unsigned lb = la + TILE * 4u;
+        if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false>(ba2, d.lda2, k0 - d.k1, la);
+        else buf_tile<A_KM>(ba, d.lda, k0, la);
+        buf_tile<B_KM>(bb, d.ldb, k0, lb);
     };
 
     if constexpr (PRO_IN_LDS) {   // visible after the first loop barrier
@@ -884,6 +906,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             // ---- prologues (previous layer's BN+ReLU) and the K tail, on the fragments
             if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
                 if (pro_step) {
+#if URED_PRO_PACKED
                     // the two M-halves share channel j: one packed fma (v_pk_fma_f32) per pair
 #pragma unroll
                     for (int j = 0; j < 16; ++j) {
@@ -894,6 +917,14 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                         if (PRO_A == URED_PRO_ENC) v = (f2v){fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
                         a[0][j] = v.x; a[1][j] = v.y;
                     }
+#else
+                    // scalar v_fma_f32 + v_max_f32: beside MFMAs a packed v_pk_fma_f32 costs more
+                    // issue time than two plain fmas (MI355X_MICROARCH.md, filler prices)
+#pragma unroll
+                    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) a[tm][j] = pro_v<PRO_A>(a[tm][j], ss[j], tt[j]);
+#endif
                 }
             }
             if constexpr (B_KM && PRO_B != URED_PRO_NONE) {
@@ -942,7 +973,8 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
 // out[m][n] (+)= sum_z ws[z][m][n]. Block = 64 consecutive elements x 4 waves; wave w sums
 // splits w, w+4, ... with four independent accumulators; fixed combine order (deterministic).
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
-                                                            float* __restrict__ out, int ldo, int accumulate) {
+                                                            float* __restrict__ out, int ldo, int accumulate,
+                                                            const float* __restrict__ bias) {
     __shared__ float part[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const size_t total = (size_t)M * N;
@@ -961,8 +993,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     part[w][lane] = (a0 + a1) + (a2 + a3);
     __syncthreads();
     if (w == 0 && e < total) {
-        const float sum = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
         const int m = (int)(e / N), n = (int)(e % N);
+        const float sum = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]) + (bias ? bias[n] : 0.f);
         float* o = out + (size_t)m * ldo + n;
         *o = accumulate ? *o + sum : sum;
     }
@@ -1316,6 +1348,9 @@ int dispatch(const UredGemmDesc& d, hipStream_t st) {
         // dgrad
         URED_CASE(0, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_BNBWD)
         URED_CASE(0, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_STORE)
+        // few output tiles, long K (per-group codes, fc layers): split-K partials
+        URED_CASE(0, 0, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_SPLITK)
+        URED_CASE(0, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_SPLITK)
         // wgrad (split-K over points)
         URED_CASE(1, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_SPLITK)
         URED_CASE(1, 1, URED_PRO_NONE, URED_PRO_ENC, URED_EPI_SPLITK)
@@ -1361,7 +1396,8 @@ int ured_gemm(const UredGemmDesc* dp, void* stream) {
     return ured::launch_status("ured_gemm");
 }
 
-int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, int ldo, int accumulate, void* stream) {
+int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, int ldo, int accumulate,
+                       const float* bias, void* stream) {
     ured::clear_error();
     URED_REQUIRE(splits >= 1 && M >= 0 && N >= 0 && ldo >= N, "ured_splitk_reduce: bad sizes");
     if (M == 0 || N == 0) return 0;
@@ -1369,7 +1405,7 @@ int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, in
     const size_t total = (size_t)M * N;
     URED_REQUIRE((total + 63) / 64 <= 0x7fffffff, "ured_splitk_reduce: too many elements");
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
-                       ws, splits, M, N, out, ldo, accumulate);
+                       ws, splits, M, N, out, ldo, accumulate, bias);
     return ured::launch_status("ured_splitk_reduce");
 }
 

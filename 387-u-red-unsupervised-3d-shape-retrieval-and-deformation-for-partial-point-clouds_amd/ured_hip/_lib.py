@@ -12,7 +12,8 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libured_hip.so"
-LIB_PATH = os.path.join(_HERE, LIB_NAME)
+# URED_LIB: an alternative build of the same ABI (A/B kernel experiments, tools/)
+LIB_PATH = os.environ.get("URED_LIB") or os.path.join(_HERE, LIB_NAME)
 ABI_VERSION = 2
 
 _P = ctypes.c_void_p

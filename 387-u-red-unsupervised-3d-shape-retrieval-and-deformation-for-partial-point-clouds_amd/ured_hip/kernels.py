@@ -31,7 +31,7 @@ class GemmDesc(ctypes.Structure):
 
 _SIGS = {
     "ured_gemm": [ctypes.POINTER(GemmDesc), _P],
-    "ured_splitk_reduce": [_P, _I, _I, _I, _P, _I, _I, _P],
+    "ured_splitk_reduce": [_P, _I, _I, _I, _P, _I, _I, _P, _P],
     "ured_bn_fwd_finalize": [_P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "ured_bn_bwd_finalize": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P],
     "ured_bn_bwd_apply": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
@@ -61,7 +61,18 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro
          rowbias=None, ldr=0, gidx=None, group_rows=0, stat_relu=False, stat_ws=None, pool_ws=None,
          Yp=None, ldy=0, bn=None, bwd_res=False, pool_idx=None, pool_grad=None, pool_group_rows=0,
          bwd_ws=None, splits=1, gadd=None, ldg=0):
-    """One ured_gemm launch. Offsets are in elements of the respective tensor."""
+    """One ured_gemm launch (two when a plain store GEMM with few output tiles and a long K is
+    split over K: split-K partials + a reduce that adds the bias). Offsets are in elements."""
+    if (epi == EPI_STORE and pro_a == PRO_NONE and pro_b == PRO_NONE and A2 is None and not a_kmajor
+            and K >= 512):
+        tiles = ((M + BM - 1) // BM) * ((N + BM - 1) // BM)
+        if tiles <= 16:
+            sp = min(1024 // tiles, K // 128)
+            ws = torch.empty(sp, M, N, device=C.device)
+            gemm(M, N, K, A, lda, B, ldb, ws, N, b_kmajor=b_kmajor, epi=EPI_SPLITK, splits=sp,
+                 A_off=A_off, B_off=B_off)
+            splitk_reduce(ws, sp, M, N, C, ldc, False, C_off, bias=bias)
+            return
     d = GemmDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
     d.a_kmajor, d.b_kmajor, d.pro_a, d.pro_b, d.epi = int(a_kmajor), int(b_kmajor), pro_a, pro_b, epi
@@ -191,14 +202,18 @@ def colsum(X):
     return group_colsum(X, N, 1, group_rows=R)[0]
 
 
-def splitk_reduce(ws, splits, M, N, out, ldo, accumulate=False, out_off=0):
+def splitk_reduce(ws, splits, M, N, out, ldo, accumulate=False, out_off=0, bias=None):
     _lib.call("ured_splitk_reduce", _p(ws), int(splits), int(M), int(N), _addr(out, out_off), int(ldo),
-              int(bool(accumulate)), _lib.stream_of(out))
+              int(bool(accumulate)), _p(bias), _lib.stream_of(out))
 
 
 def choose_splits(Mo, No, K):
+    """Split-K factor of a weight gradient (K = points): about 1024 workgroups in total, at
+    least 512 points per split (128 for outputs of <= 4 tiles, whose few workgroups would
+    otherwise each walk hundreds of K-steps), at most 256 splits."""
     tiles = ((Mo + 127) // 128) * ((No + 127) // 128)
-    s = max(1, min(1024 // max(tiles, 1), K // 512))
+    min_k = 128 if tiles <= 4 else 512
+    s = max(1, min(1024 // max(tiles, 1), K // min_k))
     return max(1, min(s, 256))
 
 

@@ -153,8 +153,10 @@ typedef struct UredGemmDesc {
 
 int ured_gemm(const UredGemmDesc* d, void* stream);
 
-/* Sum split-K partials: out[m][n] = (accumulate ? out : 0) + sum_z ws[z][m][n] (z ascending). */
-int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, int ldo, int accumulate, void* stream);
+/* Sum split-K partials: out[m][n] = (accumulate ? out : 0) + sum_z ws[z][m][n] (+ bias[n] if non-NULL);
+ * fixed combine order (deterministic). */
+int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, int ldo, int accumulate,
+                       const float* bias, void* stream);
 
 /* BN forward finalize over the per-block partials of EPI_FWD (M rows, blocks of 128):
  * fp64 Chan merge -> mean, invstd = 1/sqrt(var_biased+eps), scale = gamma*invstd,
