@@ -285,6 +285,279 @@ int fwd_dispatch(const NNFwdArgs& a, int nseg, int max_a, int max_b, hipStream_t
     return 0;
 }
 
+// ---- fused forward: both directions from ONE evaluation of every distance -----------------
+// The two-pass kernel above evaluates each pair twice (once per direction). Here a wave holds
+// QPT queries (a-points) per lane in registers (64*QPT per wave, contiguous per lane) and
+// streams a range of refs (b-points) through its own LDS tile; each distance feeds
+//   * the query's running row minimum (in-lane v_min3, chunk-of-16 tracking as above), and
+//   * the ref's column minimum: in-lane over the lane's QPT queries, then across the wave
+//     (4 DPP steps + 4 readlanes on the float bits — distances are >= 0, so the unsigned
+//     order is the float order), and the FIRST lane holding that minimum by a ballot.
+// Each wave stores, per ref / per query, a 64-bit key (value bits << 32 | tag) into a
+// workspace slab (one slot per (q-tile, ref) and per (ref-range, query); plain stores, no
+// atomics); nn_fused_finalize takes the lexicographic minimum over the slab (lowest tag
+// on equal values = lowest chunk / lowest query group) and rescans that one chunk (16 refs)
+// or query group (QPT queries) for the first index with d == min: the reference's
+// lowest-index tie rule, exactly, with every distance evaluated by the contract formula.
+constexpr int NF_TILE = 512;    // refs per LDS fill (per wave, 6 KiB SoA)
+constexpr int NF_TARGET_WAVES = 4096;
+
+struct NNFusedArgs {
+    const float* a; const float* b; const int4* segs;
+    int n, m;                    // dense mode sizes
+    int qtiles, rsplit, rr;      // grid.x = qtiles * rsplit; rr refs per range (multiple of 16)
+    int a_total, b_total;        // slab strides
+    unsigned long long* rowslab; // [rsplit][a_total]
+    unsigned long long* colslab; // [qtiles][b_total]
+    float* dist_a; int* idx_a; float* dist_b; int* idx_b;
+};
+
+__device__ __forceinline__ void seg_of(const NNFusedArgs& A, int s, int& ao, int& al, int& bo, int& bl) {
+    if (A.segs) { const int4 q = A.segs[s]; ao = q.x; al = q.y; bo = q.z; bl = q.w; }
+    else { ao = s * A.n; al = A.n; bo = s * A.m; bl = A.m; }
+}
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ unsigned dpp_min(unsigned v) {
+    // full-row patterns: every lane has a source (foldable into v_min_u32_dpp);
+    // row_bcast with a row mask: rows outside the mask keep v (old = v)
+    const unsigned o = ROW_MASK == 0xF
+        ? (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true)
+        : (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xF, false);
+    return v < o ? v : o;
+}
+
+// s_min_u32 on wave-uniform values (hipcc otherwise moves them to VGPRs for a v_min3_u32).
+__device__ __forceinline__ unsigned smin(unsigned a, unsigned b) {
+    unsigned r;
+    asm("s_min_u32 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b));
+    return r;
+}
+
+// Minimum over the 64 lanes of each of four values, as wave-uniform (SGPR) results. Four
+// independent DPP chains interleaved (no hazard nops) make each value uniform within its row
+// of 16 lanes; four readlanes and scalar mins finish the reduction.
+__device__ __forceinline__ void wave_min4(unsigned (&v)[4], unsigned (&w)[4]) {
+#define URED_STEP(C) _Pragma("unroll") for (int k = 0; k < 4; ++k) v[k] = dpp_min<C, 0xF>(v[k]);
+    URED_STEP(0xB1)    // quad_perm [1,0,3,2]
+    URED_STEP(0x4E)    // quad_perm [2,3,0,1]
+    URED_STEP(0x141)   // row_half_mirror
+    URED_STEP(0x140)   // row_mirror
+#undef URED_STEP
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const unsigned r0 = (unsigned)__builtin_amdgcn_readlane((int)v[k], 0);
+        const unsigned r1 = (unsigned)__builtin_amdgcn_readlane((int)v[k], 16);
+        const unsigned r2 = (unsigned)__builtin_amdgcn_readlane((int)v[k], 32);
+        const unsigned r3 = (unsigned)__builtin_amdgcn_readlane((int)v[k], 48);
+        w[k] = smin(smin(r0, r1), smin(r2, r3));
+    }
+}
+
+// v_writelane_b32: lane `sel` of dst := src (both scalar); no builtin in this toolchain. The
+// lane select goes through m0 (one SGPR operand per VALU instruction: constant-bus limit),
+// with one wait state after the m0 write.
+__device__ __forceinline__ unsigned writelane(unsigned dst, unsigned src, int sel) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0" : "+v"(dst) : "s"(src), "s"(sel) : "m0");
+    return dst;
+}
+
+template <int QPT>
+__global__ __launch_bounds__(64) void nn_fused_kernel(NNFusedArgs A) {
+    // refs stored replicated ({x,x}) so one LDS read feeds both halves of a packed op whose
+    // other operand is a pair of queries: queries then need no replicated registers.
+    __shared__ __attribute__((aligned(16))) f2 sx[NF_TILE];
+    __shared__ __attribute__((aligned(16))) f2 sy[NF_TILE];
+    __shared__ __attribute__((aligned(16))) f2 sz[NF_TILE];
+    constexpr int QP = QPT / 2;
+    const int s = blockIdx.y;
+    const int qt = blockIdx.x % A.qtiles, rs = blockIdx.x / A.qtiles;
+    int ao, al, bo, bl;
+    seg_of(A, s, ao, al, bo, bl);
+    const int q0 = qt * 64 * QPT;
+    const int r_begin = rs * A.rr;
+    if (q0 >= al || r_begin >= bl) return;   // wave-uniform
+    const int r_end = min(bl, r_begin + A.rr);
+    const int lane = threadIdx.x;
+
+    f2 qx[QP], qy[QP], qz[QP];               // queries 2j, 2j+1 of this lane
+    float best[QPT];
+    int bchunk[QPT];
+#pragma unroll
+    for (int i = 0; i < QPT; ++i) {
+        const int qi = q0 + lane * QPT + i;
+        float x = NN_PAD, y = NN_PAD, z = NN_PAD;   // padded queries: d = +inf to every ref
+        if (qi < al) {
+            const float* p = A.a + 3 * (size_t)(ao + qi);
+            x = p[0]; y = p[1]; z = p[2];
+        }
+        if (i & 1) { qx[i >> 1].y = x; qy[i >> 1].y = y; qz[i >> 1].y = z; }
+        else       { qx[i >> 1].x = x; qy[i >> 1].x = y; qz[i >> 1].x = z; }
+        best[i] = __builtin_inff();
+        bchunk[i] = 0;
+    }
+    unsigned long long* colslab = A.colslab + (size_t)qt * A.b_total + bo;
+    const int qgroup0 = q0 / QPT;
+
+    for (int t0 = r_begin; t0 < r_end; t0 += NF_TILE) {
+        const int tn = min(NF_TILE, r_end - t0);
+        __syncthreads();
+        for (int k = lane; k < ((tn + 15) & ~15); k += 64) {
+            float x = NN_PAD, y = NN_PAD, z = NN_PAD;
+            if (k < tn) {
+                const float* p = A.b + 3 * (size_t)(bo + t0 + k);
+                x = p[0]; y = p[1]; z = p[2];
+            }
+            sx[k] = f2{x, x}; sy[k] = f2{y, y}; sz[k] = f2{z, z};
+        }
+        __syncthreads();
+        const int nch = (tn + 15) >> 4;
+        for (int c = 0; c < nch; ++c) {
+            float mn[QPT];
+#pragma unroll
+            for (int i = 0; i < QPT; ++i) mn[i] = __builtin_inff();
+            unsigned klo = 0, khi = 0;   // lane k < 16: column key of ref k of this chunk
+#pragma unroll 1
+            for (int p = 0; p < 16; p += 4) {
+                f2 rx[4], ry[4], rz[4];
+#pragma unroll
+                for (int h = 0; h < 4; ++h) { rx[h] = sx[c * 16 + p + h]; ry[h] = sy[c * 16 + p + h]; rz[h] = sz[c * 16 + p + h]; }
+                float cm[4] = {__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff()};
+#pragma unroll
+                for (int j = 0; j < QP; ++j) {
+                    f2 d[4];
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        const f2 dx = rx[h] - qx[j], dy = ry[h] - qy[j], dz = rz[h] - qz[j];
+                        f2 e = dx * dx;
+                        e = __builtin_elementwise_fma(dy, dy, e);
+                        d[h] = __builtin_elementwise_fma(dz, dz, e);
+                    }
+                    mn[2 * j] = __builtin_fminf(__builtin_fminf(mn[2 * j], d[0].x), d[1].x);
+                    mn[2 * j] = __builtin_fminf(__builtin_fminf(mn[2 * j], d[2].x), d[3].x);
+                    mn[2 * j + 1] = __builtin_fminf(__builtin_fminf(mn[2 * j + 1], d[0].y), d[1].y);
+                    mn[2 * j + 1] = __builtin_fminf(__builtin_fminf(mn[2 * j + 1], d[2].y), d[3].y);
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) cm[h] = __builtin_fminf(__builtin_fminf(cm[h], d[h].x), d[h].y);
+                }
+                // column keys of refs p .. p+3: wave minimum + first lane holding it
+                const unsigned v[4] = {__float_as_uint(cm[0]), __float_as_uint(cm[1]),
+                                       __float_as_uint(cm[2]), __float_as_uint(cm[3])};
+                unsigned t[4] = {v[0], v[1], v[2], v[3]}, w[4];
+                wave_min4(t, w);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const unsigned tag = (unsigned)qgroup0 + (unsigned)__builtin_ctzll(__ballot(v[k] == w[k]));
+                    klo = writelane(klo, tag, p + k);
+                    khi = writelane(khi, w[k], p + k);
+                }
+            }
+            const int gc = (t0 + c * 16) >> 4;       // chunk index within the segment's refs
+#pragma unroll
+            for (int i = 0; i < QPT; ++i)
+                if (mn[i] < best[i]) { best[i] = mn[i]; bchunk[i] = gc; }
+            const int r = t0 + c * 16 + lane;
+            if (lane < 16 && r < r_end)
+                colslab[r] = ((unsigned long long)khi << 32) | klo;
+        }
+    }
+    unsigned long long* rowslab = A.rowslab + (size_t)rs * A.a_total + ao;
+#pragma unroll
+    for (int i = 0; i < QPT; ++i) {
+        const int qi = q0 + lane * QPT + i;
+        if (qi < al) rowslab[qi] = ((unsigned long long)__float_as_uint(best[i]) << 32) | (unsigned)bchunk[i];
+    }
+}
+
+// One thread per point of either side: lexicographic min over the slab, then the exact rescan.
+template <int QPT>
+__global__ __launch_bounds__(256) void nn_fused_finalize(NNFusedArgs A) {
+    const int s = blockIdx.y, dir = blockIdx.z;
+    int ao, al, bo, bl;
+    seg_of(A, s, ao, al, bo, bl);
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (dir == 0) {
+        if (j >= al) return;
+        if (bl <= 0) { A.dist_a[ao + j] = 0.f; A.idx_a[ao + j] = 0; return; }
+        const int nrs = (bl + A.rr - 1) / A.rr;
+        unsigned long long key = ~0ull;
+        for (int r = 0; r < nrs; ++r) {
+            const unsigned long long k = A.rowslab[(size_t)r * A.a_total + ao + j];
+            key = k < key ? k : key;
+        }
+        const float v = __uint_as_float((unsigned)(key >> 32));
+        const int k0 = (int)(unsigned)key * 16, kn = min(16, bl - k0);
+        const float* q = A.a + 3 * (size_t)(ao + j);
+        int bi = k0;
+        for (int k = 0; k < kn; ++k) {
+            const float* p = A.b + 3 * (size_t)(bo + k0 + k);
+            if (sqd(q[0], q[1], q[2], p[0], p[1], p[2]) == v) { bi = k0 + k; break; }
+        }
+        A.dist_a[ao + j] = v;
+        A.idx_a[ao + j] = bi;
+    } else {
+        if (j >= bl) return;
+        if (al <= 0) { A.dist_b[bo + j] = 0.f; A.idx_b[bo + j] = 0; return; }
+        const int nqt = (al + 64 * QPT - 1) / (64 * QPT);
+        unsigned long long key = ~0ull;
+        for (int t = 0; t < nqt; ++t) {
+            const unsigned long long k = A.colslab[(size_t)t * A.b_total + bo + j];
+            key = k < key ? k : key;
+        }
+        const float v = __uint_as_float((unsigned)(key >> 32));
+        const int k0 = (int)(unsigned)key * QPT, kn = min(QPT, al - k0);
+        const float* p = A.b + 3 * (size_t)(bo + j);
+        int bi = k0;
+        for (int k = 0; k < kn; ++k) {
+            const float* q = A.a + 3 * (size_t)(ao + k0 + k);
+            if (sqd(q[0], q[1], q[2], p[0], p[1], p[2]) == v) { bi = k0 + k; break; }
+        }
+        A.dist_b[bo + j] = v;
+        A.idx_b[bo + j] = bi;
+    }
+}
+
+// Grid plan of the fused path (host-only arithmetic; also sizes the workspace).
+struct FusedPlan { int qpt, qtiles, rsplit, rr; size_t ws_bytes; };
+
+FusedPlan fused_plan(int nseg, int max_a, int max_b, int a_total, int b_total) {
+    FusedPlan p{};
+    if (nseg <= 0 || max_a <= 0 || max_b <= 0) return p;
+    const long long pairs = (long long)nseg * max_a * max_b;
+    p.qpt = (pairs >= (1ll << 28) && max_a >= 1024) ? 16 : 8;
+    const int qtile = 64 * p.qpt;
+    p.qtiles = (max_a + qtile - 1) / qtile;
+    const long long base = (long long)nseg * p.qtiles;
+    long long rs = (NF_TARGET_WAVES + base - 1) / base;
+    const long long rs_max = (max_b + 63) / 64;         // at least 64 refs per wave
+    rs = rs < 1 ? 1 : (rs > rs_max ? rs_max : rs);
+    int rr = (int)((max_b + rs - 1) / rs);
+    rr = (rr + 15) & ~15;
+    p.rr = rr;
+    p.rsplit = (max_b + rr - 1) / rr;
+    p.ws_bytes = 8ull * ((size_t)p.rsplit * (size_t)a_total + (size_t)p.qtiles * (size_t)b_total);
+    return p;
+}
+
+int fused_dispatch(NNFusedArgs a, int nseg, int max_a, int max_b, void* ws, size_t ws_bytes, hipStream_t st) {
+    const FusedPlan p = fused_plan(nseg, max_a, max_b, a.a_total, a.b_total);
+    if (p.qpt == 0) return -1;   // not applicable: the caller runs the two-pass kernel
+    URED_REQUIRE(ws && ws_bytes >= p.ws_bytes, "nn fused: workspace of %zu bytes needed (got %zu)", p.ws_bytes, ws_bytes);
+    URED_REQUIRE((long long)p.qtiles * p.rsplit < (1ll << 31), "nn fused: grid too large");
+    a.qtiles = p.qtiles; a.rsplit = p.rsplit; a.rr = p.rr;
+    a.rowslab = reinterpret_cast<unsigned long long*>(ws);
+    a.colslab = a.rowslab + (size_t)p.rsplit * a.a_total;
+    const dim3 grid(p.qtiles * p.rsplit, nseg), fgrid((max(max_a, max_b) + 255) / 256, nseg, 2);
+    if (p.qpt == 16) {
+        hipLaunchKernelGGL(nn_fused_kernel<16>, grid, dim3(64), 0, st, a);
+        hipLaunchKernelGGL(nn_fused_finalize<16>, fgrid, dim3(256), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(nn_fused_kernel<8>, grid, dim3(64), 0, st, a);
+        hipLaunchKernelGGL(nn_fused_finalize<8>, fgrid, dim3(256), 0, st, a);
+    }
+    return 0;
+}
+
 int bwd_dispatch(const NNBwdArgs& a, int nseg, int max_a, int max_b, hipStream_t st) {
     const int max_p = max(max_a, max_b);
     if (max_p <= 0 || nseg <= 0) return 0;
@@ -370,6 +643,53 @@ int ured_nn_fwd(const float* xyz1, const float* xyz2, int b, int n, int m, int d
     NNFwdArgs a{xyz1, xyz2, nullptr, n, m, dirs, dist1, idx1, dist2, idx2};
     fwd_dispatch(a, b, n, m, (hipStream_t)stream);
     return ured::launch_status("ured_nn_fwd");
+}
+
+size_t ured_nn_fwd_workspace(int nseg, int max_a_len, int max_b_len, int a_total, int b_total, int dirs) {
+    if (dirs != 3 || nseg <= 0 || max_a_len <= 0 || max_b_len <= 0 || a_total < 0 || b_total < 0) return 0;
+    return fused_plan(nseg, max_a_len, max_b_len, a_total, b_total).ws_bytes;
+}
+
+int ured_nn_fwd_ws(const float* xyz1, const float* xyz2, int b, int n, int m, int dirs,
+                   float* dist1, int* idx1, float* dist2, int* idx2, void* workspace, size_t ws_bytes,
+                   void* stream) {
+    if (dirs != 3 || !workspace)
+        return ured_nn_fwd(xyz1, xyz2, b, n, m, dirs, dist1, idx1, dist2, idx2, stream);
+    ured::clear_error();
+    URED_REQUIRE(b >= 0 && n >= 0 && m >= 0, "ured_nn_fwd_ws: negative size (b=%d n=%d m=%d)", b, n, m);
+    URED_REQUIRE(b <= 65535, "ured_nn_fwd_ws: b %d exceeds 65535", b);
+    if (b == 0 || n == 0 || m == 0)
+        return ured_nn_fwd(xyz1, xyz2, b, n, m, dirs, dist1, idx1, dist2, idx2, stream);
+    URED_REQUIRE(xyz1 && xyz2 && dist1 && idx1 && dist2 && idx2, "ured_nn_fwd_ws: null pointer");
+    URED_REQUIRE((long long)b * n < (1ll << 31) && (long long)b * m < (1ll << 31), "ured_nn_fwd_ws: too many points");
+    NNFusedArgs a{xyz1, xyz2, nullptr, n, m, 0, 0, 0, b * n, b * m, nullptr, nullptr, dist1, idx1, dist2, idx2};
+    const int rc = fused_dispatch(a, b, n, m, workspace, ws_bytes, (hipStream_t)stream);
+    if (rc == -1) return ured_nn_fwd(xyz1, xyz2, b, n, m, dirs, dist1, idx1, dist2, idx2, stream);
+    if (rc) return rc;
+    return ured::launch_status("ured_nn_fwd_ws");
+}
+
+int ured_nn_seg_fwd_ws(const float* a, const float* b, const int* segs, int nseg,
+                       int max_a_len, int max_b_len, int dirs, int a_total, int b_total,
+                       float* dist_a, int* idx_a, float* dist_b, int* idx_b,
+                       void* workspace, size_t ws_bytes, void* stream) {
+    if (dirs != 3 || !workspace)
+        return ured_nn_seg_fwd(a, b, segs, nseg, max_a_len, max_b_len, dirs, dist_a, idx_a, dist_b, idx_b, stream);
+    ured::clear_error();
+    URED_REQUIRE(nseg >= 0 && max_a_len >= 0 && max_b_len >= 0 && a_total >= 0 && b_total >= 0,
+                 "ured_nn_seg_fwd_ws: negative size");
+    URED_REQUIRE(nseg <= 65535, "ured_nn_seg_fwd_ws: nseg %d exceeds 65535", nseg);
+    if (nseg == 0) return 0;
+    URED_REQUIRE(a && b && segs && dist_a && idx_a && dist_b && idx_b, "ured_nn_seg_fwd_ws: null pointer");
+    if (max_a_len == 0 || max_b_len == 0)   // only "empty other side" pairs: the two-pass path writes them
+        return ured_nn_seg_fwd(a, b, segs, nseg, max_a_len, max_b_len, dirs, dist_a, idx_a, dist_b, idx_b, stream);
+    NNFusedArgs A{a, b, reinterpret_cast<const int4*>(segs), 0, 0, 0, 0, 0, a_total, b_total, nullptr, nullptr,
+                  dist_a, idx_a, dist_b, idx_b};
+    const int rc = fused_dispatch(A, nseg, max_a_len, max_b_len, workspace, ws_bytes, (hipStream_t)stream);
+    if (rc == -1)
+        return ured_nn_seg_fwd(a, b, segs, nseg, max_a_len, max_b_len, dirs, dist_a, idx_a, dist_b, idx_b, stream);
+    if (rc) return rc;
+    return ured::launch_status("ured_nn_seg_fwd_ws");
 }
 
 int ured_nn_bwd(const float* xyz1, const float* xyz2, int b, int n, int m,

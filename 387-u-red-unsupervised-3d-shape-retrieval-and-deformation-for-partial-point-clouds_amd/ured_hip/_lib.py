@@ -19,15 +19,22 @@ ABI_VERSION = 2
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
+_SZ = ctypes.c_size_t
 
 # name -> argtypes (all functions return int status, 0 = ok)
 _SIGNATURES = {
     "ured_nn_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_nn_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "ured_nn_seg_fwd": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "ured_nn_fwd_workspace": [_I, _I, _I, _I, _I, _I],
+    "ured_nn_fwd_ws": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _SZ, _P],
+    "ured_nn_seg_fwd_ws": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _SZ, _P],
     "ured_nn_seg_bwd": [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "ured_dcd": [_P, _P, _P, _P, _I, _I, _I, _F, _I, _F, _F, _P, _P, _P, _P],
 }
+
+# entry points that return a value instead of a status (see query())
+_RESTYPES = {"ured_nn_fwd_workspace": _SZ}
 
 _lib = None
 
@@ -56,7 +63,7 @@ def lib():
     for name, argtypes in _SIGNATURES.items():
         fn = getattr(handle, name)
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_int
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
     _lib = handle
     return _lib
 
@@ -82,6 +89,11 @@ def call(name, *args):
     if rc != 0:
         msg = handle.ured_last_error().decode(errors="replace")
         raise UredError(f"{name} failed (status {rc}): {msg}")
+
+
+def query(name, *args):
+    """Call a value-returning entry point (e.g. a workspace size query)."""
+    return getattr(lib(), name)(*args)
 
 
 def ptr(t):

@@ -11,6 +11,24 @@ from torch.autograd import Function
 
 from . import _lib
 
+# Both directions from one evaluation of every pair distance (ured_nn_fwd_ws /
+# ured_nn_seg_fwd_ws). Results are bit-identical to the two-pass kernel; the switch exists
+# so the tests can run both paths.
+FUSED = True
+# Below ~1e8 pairs a launch is latency-bound and the two-pass kernel (one launch, no
+# finalize) is faster on MI355X (16x2048x2048: 30 vs 39 us); from there up the fused one
+# (64x4096x4096: 1.27x, ragged 16x16384x2048: 4.3x, 4096x1024x1024: 1.15x).
+FUSED_MIN_PAIRS = 96 << 20
+
+
+def _workspace(nseg, max_a, max_b, a_total, b_total, dirs, dev):
+    if not FUSED or nseg * max_a * max_b < FUSED_MIN_PAIRS:
+        return None, 0
+    nbytes = _lib.query("ured_nn_fwd_workspace", nseg, max_a, max_b, a_total, b_total, dirs)
+    if nbytes == 0:
+        return None, 0
+    return torch.empty(nbytes, dtype=torch.uint8, device=dev), nbytes
+
 
 def _as_points(t, name):
     if t.dtype != torch.float32:
@@ -40,9 +58,10 @@ class NNDenseFunction(Function):
         if n == 0 or m == 0:
             dist1.zero_(); dist2.zero_(); idx1.zero_(); idx2.zero_()
         else:
-            _lib.call("ured_nn_fwd", _lib.ptr(xyz1), _lib.ptr(xyz2), b, n, m, 3,
+            ws, nbytes = _workspace(b, n, m, b * n, b * m, 3, dev)
+            _lib.call("ured_nn_fwd_ws", _lib.ptr(xyz1), _lib.ptr(xyz2), b, n, m, 3,
                       _lib.ptr(dist1), _lib.ptr(idx1), _lib.ptr(dist2), _lib.ptr(idx2),
-                      _lib.stream_of(xyz1))
+                      _lib.ptr(ws), nbytes, _lib.stream_of(xyz1))
         ctx.save_for_backward(xyz1, xyz2, idx1, idx2)
         ctx.mark_non_differentiable(idx1, idx2)
         return dist1, dist2, idx1, idx2
@@ -87,10 +106,11 @@ class NNSegFunction(Function):
         idx_b = torch.zeros(b.shape[0], device=dev, dtype=torch.int32)
         nseg = segs.shape[0]
         if nseg:
-            _lib.call("ured_nn_seg_fwd", _lib.ptr(a), _lib.ptr(b), _lib.ptr(segs), nseg,
-                      int(max_a), int(max_b), int(dirs),
+            ws, nbytes = _workspace(nseg, int(max_a), int(max_b), a.shape[0], b.shape[0], int(dirs), dev)
+            _lib.call("ured_nn_seg_fwd_ws", _lib.ptr(a), _lib.ptr(b), _lib.ptr(segs), nseg,
+                      int(max_a), int(max_b), int(dirs), a.shape[0], b.shape[0],
                       _lib.ptr(dist_a), _lib.ptr(idx_a), _lib.ptr(dist_b), _lib.ptr(idx_b),
-                      _lib.stream_of(a))
+                      _lib.ptr(ws), nbytes, _lib.stream_of(a))
         ctx.save_for_backward(a, b, segs, idx_a, idx_b)
         ctx.max_a, ctx.max_b, ctx.dirs = int(max_a), int(max_b), int(dirs)
         ctx.mark_non_differentiable(idx_a, idx_b)

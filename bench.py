@@ -168,11 +168,14 @@ def cpu_baseline(args, cfg_small_threads=16):
                       f"N={args.points} on {threads} host threads, {dt:.1f} s"}
 
 
-def chamfer_rate(dev, iters=20):
+def chamfer_rate(dev, B=16, n=2048, m=2048, iters=20):
+    """NN forward (both directions) on one dense [B,n,3] x [B,m,3] call: Gpair-dist/s and the
+    two SURVEY §8(d) roofline fractions (8 FLOP/pair vs 157.3 TFLOP/s FP32 VALU — the binding
+    roof; 12 B/point read vs 8 TB/s HBM — the north star's, unattainable by construction)."""
     from ured_hip import nn as unn
     g = torch.Generator().manual_seed(0)
-    p1 = torch.rand(16, 2048, 3, generator=g).to(dev)
-    p2 = torch.rand(16, 2048, 3, generator=g).to(dev)
+    p1 = torch.rand(B, n, 3, generator=g).to(dev)
+    p2 = torch.rand(B, m, 3, generator=g).to(dev)
     for _ in range(3):
         unn.nn_dense(p1, p2)
     torch.cuda.synchronize()
@@ -183,7 +186,11 @@ def chamfer_rate(dev, iters=20):
     e1.record()
     torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / iters * 1e-3
-    return 16 * 2048 * 2048 / t / 1e9
+    pairs = B * n * m
+    return {"shape": f"{B}x{n}x{m}", "ms": round(t * 1e3, 4), "gpair_dist_s": round(pairs / t / 1e9, 1),
+            "path": "fused" if pairs >= unn.FUSED_MIN_PAIRS else "two-pass",
+            "valu_frac": round(8 * pairs / t / 157.3e12, 4),
+            "hbm_read_frac": round(12 * B * (n + m) / t / 8e12, 6)}
 
 
 def pair_rate(dev, parts=512, pts=1024):
@@ -377,7 +384,9 @@ def main():
     if all_slots_rate is not None:
         extra["all_slots_iters_s"] = round(all_slots_rate, 4)
     extra["unique_sources"] = bool(cfg["unique_sources"])
-    extra["chamfer_gpair_s"] = round(chamfer_rate(dev), 1)
+    ch = chamfer_rate(dev)
+    extra["chamfer_gpair_s"] = ch["gpair_dist_s"]
+    extra["chamfer"] = [ch, chamfer_rate(dev, 64, 4096, 4096, iters=10), chamfer_rate(dev, 16, 16384, 2048, iters=10)]
     extra["pseudo_label_dcd"] = pair_rate(dev)
     extra["loss"] = loss_val
     cpu = None if args.no_cpu_baseline else cpu_baseline(args)

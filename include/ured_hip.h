@@ -20,6 +20,7 @@
  *                       (Shape_Measure ChamferLoss calls) and
  *                       loss/basic_loss.py:249-265 (pytorch3d knn_points K=1),
  *                       batched into one ragged launch.
+ *   ured_nn_fwd_ws / ured_nn_seg_fwd_ws <- the same two, both directions in one pass
  *   ured_nn_seg_bwd  <- autograd of the above (NmDistanceGradKernel semantics,
  *                       chamfer3D.cu:155-174, made deterministic).
  */
@@ -69,6 +70,22 @@ int ured_nn_bwd(const float* xyz1, const float* xyz2, int b, int n, int m,
 int ured_nn_seg_fwd(const float* a, const float* b, const int* segs, int nseg,
                     int max_a_len, int max_b_len, int dirs,
                     float* dist_a, int* idx_a, float* dist_b, int* idx_b, void* stream);
+
+/* Fused forward (both directions from ONE evaluation of every pair distance; same results,
+ * bit for bit, as ured_nn_fwd / ured_nn_seg_fwd with dirs = 3). The caller passes a device
+ * workspace of ured_nn_fwd_workspace(...) bytes (no initialisation needed; contents are
+ * scratch). a_total / b_total = number of points in the a / b buffers (dense: b*n, b*m).
+ * ured_nn_fwd_workspace returns 0 when the fused path does not apply (dirs != 3, empty
+ * sizes); the _ws entry points then (or with workspace == NULL) run the two-pass kernel. */
+#include <stddef.h>
+size_t ured_nn_fwd_workspace(int nseg, int max_a_len, int max_b_len, int a_total, int b_total, int dirs);
+int ured_nn_fwd_ws(const float* xyz1, const float* xyz2, int b, int n, int m, int dirs,
+                   float* dist1, int* idx1, float* dist2, int* idx2, void* workspace, size_t ws_bytes,
+                   void* stream);
+int ured_nn_seg_fwd_ws(const float* a, const float* b, const int* segs, int nseg,
+                       int max_a_len, int max_b_len, int dirs, int a_total, int b_total,
+                       float* dist_a, int* idx_a, float* dist_b, int* idx_b,
+                       void* workspace, size_t ws_bytes, void* stream);
 
 /* Backward of ured_nn_seg_fwd: accumulates into ga (a-points) and gb (b-points)
  * exactly the per-pair formula of ured_nn_bwd. gd_a / gd_b may be NULL. */

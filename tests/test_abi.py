@@ -9,7 +9,7 @@ from conftest import ROOT
 
 def _declared():
     hdr = open(os.path.join(ROOT, "include", "ured_hip.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ured_\w+)\s*\(", hdr, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(ured_\w+)\s*\(", hdr, re.M)))
 
 
 def test_header_symbols_exported(built):

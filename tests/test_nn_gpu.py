@@ -19,9 +19,11 @@ def _rand(shape, seed):
     return np.random.Generator(np.random.PCG64(seed)).random(shape, dtype=np.float32)
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("b,n,m", [(4, 100, 200), (3, 257, 129), (2, 1, 5), (1, 2048, 2048), (2, 1023, 1025),
                                    (5, 3000, 17), (1, 17, 4100)])
-def test_dense_fwd_bitexact(unn, dev, b, n, m):
+def test_dense_fwd_bitexact(unn, dev, b, n, m, fused, monkeypatch):
+    monkeypatch.setattr(unn, "FUSED_MIN_PAIRS", 0 if fused else 1 << 62)
     p1, p2 = _rand((b, n, 3), n), _rand((b, m, 3), m + 7)
     d1, d2, i1, i2 = unn.nn_dense(torch.from_numpy(p1).to(dev), torch.from_numpy(p2).to(dev))
     r = nn_ref.nn_fwd(p1, p2)
@@ -163,3 +165,68 @@ def test_errors_raise(unn, dev):
         unn.nn_dense(torch.rand(2, 5, 3), torch.rand(2, 5, 3))  # CPU tensors: no fallback
     with pytest.raises(_lib.UredError):
         _lib.call("ured_nn_fwd", None, None, 1, 4, 4, 3, None, None, None, None, None)
+
+
+@pytest.fixture
+def fused_always(unn, monkeypatch):
+    """Fused path at every size (the wrapper otherwise keeps small launches two-pass)."""
+    monkeypatch.setattr(unn, "FUSED_MIN_PAIRS", 0)
+
+
+@pytest.fixture
+def two_pass(unn):
+    """Run the wrapped block with the two-pass forward (ured_nn_fwd / ured_nn_seg_fwd)."""
+    class _Ctx:
+        def __enter__(self):
+            unn.FUSED = False
+
+        def __exit__(self, *a):
+            unn.FUSED = True
+    return _Ctx()
+
+
+@pytest.mark.parametrize("b,n,m", [(8, 5000, 3000), (2, 20000, 700), (64, 1024, 1024), (3, 33, 9000)])
+def test_fused_equals_two_pass(unn, dev, fused_always, two_pass, b, n, m):
+    """The fused both-direction forward (several q-tiles and ref ranges per pair) is bitwise
+    the two-pass kernel; small sizes are checked against the C oracle directly above."""
+    g = torch.Generator(device="cpu").manual_seed(n + m)
+    p1, p2 = torch.rand(b, n, 3, generator=g).to(dev), torch.rand(b, m, 3, generator=g).to(dev)
+    fused = unn.nn_dense(p1, p2)
+    with two_pass:
+        ref = unn.nn_dense(p1, p2)
+    for x, y in zip(fused, ref):
+        assert torch.equal(x, y)
+
+
+def test_fused_column_ties_across_tiles(unn, dev, fused_always):
+    """Exact column ties between queries of different q-tiles / lanes / ref ranges: every ref
+    of a lattice has several identical query copies spread over the query range; the lowest
+    query index must win, as in the reference (chamfer3D.cu strict '<')."""
+    ax = np.linspace(0, 1, 6, dtype=np.float32)
+    grid = np.stack(np.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3)
+    rng = np.random.Generator(np.random.PCG64(5))
+    q = rng.random((6000, 3), dtype=np.float32) * 0.5 + 0.25
+    for pos in (100, 1500, 2900, 4100, 5700):      # copies in different tiles
+        q[pos:pos + len(grid)] = grid
+    refs = np.concatenate([grid, rng.random((3000, 3), dtype=np.float32)], 0)
+    for qq, rr in ((q, refs), (refs, q)):
+        d1, d2, i1, i2 = unn.nn_dense(torch.from_numpy(qq[None]).to(dev), torch.from_numpy(rr[None]).to(dev))
+        r = nn_ref.nn_fwd(qq[None], rr[None])
+        np.testing.assert_array_equal(i1.cpu().numpy(), r[2])
+        np.testing.assert_array_equal(i2.cpu().numpy(), r[3])
+        np.testing.assert_array_equal(d1.cpu().numpy(), r[0])
+        np.testing.assert_array_equal(d2.cpu().numpy(), r[1])
+
+
+def test_fused_segments_equal_two_pass(unn, dev, fused_always, two_pass):
+    """Ragged families as the train step issues them (k_b*1024 vs 2048, per-part 1024 vs
+    1024) plus empty pairs: fused == two-pass, bitwise."""
+    rng = np.random.Generator(np.random.PCG64(9))
+    segs, na, nb = _segs(rng, 0, 0, 40, 16384, 2048)
+    a, b = torch.rand(na, 3).to(dev), torch.rand(nb, 3).to(dev)
+    ts = torch.from_numpy(segs).to(dev)
+    fused = unn.nn_segments(a, b, ts, 16384, 2048, 3)
+    with two_pass:
+        ref = unn.nn_segments(a, b, ts, 16384, 2048, 3)
+    for x, y in zip(fused, ref):
+        assert torch.equal(x, y)

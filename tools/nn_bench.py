@@ -38,10 +38,13 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
     res = {}
-    for (B, n, m) in [(16, 2048, 2048), (64, 4096, 4096), (32, 2000, 1000), (16, 4096, 2048), (16, 16384, 2048)]:
+    for (B, n, m) in [(16, 2048, 2048), (64, 4096, 4096), (32, 2000, 1000), (16, 4096, 2048), (16, 16384, 2048), (4096, 1024, 1024)]:
         p1 = torch.rand(B, n, 3, generator=g).to(dev)
         p2 = torch.rand(B, m, 3, generator=g).to(dev)
         t_f = timeit(lambda: unn.nn_dense(p1, p2), a.iters)
+        unn.FUSED = False
+        t_2p = timeit(lambda: unn.nn_dense(p1, p2), a.iters)
+        unn.FUSED = True
         q1 = p1.clone().requires_grad_(True)
 
         def fb():
@@ -50,8 +53,9 @@ def main():
         t_fb = timeit(fb, a.iters)
         pairs = B * n * m
         res[f"{B}x{n}x{m}"] = {"fwd_ms": t_f * 1e3, "fwd_gpair_s": pairs / t_f / 1e9,
+                               "two_pass_fwd_ms": t_2p * 1e3, "two_pass_gpair_s": pairs / t_2p / 1e9,
                                "fwdbwd_ms": t_fb * 1e3, "fwdbwd_gpair_s": pairs / t_fb / 1e9}
-        print(f"{B}x{n}x{m}: fwd {t_f*1e3:.3f} ms ({pairs/t_f/1e9:.1f} Gpair/s)  fwd+bwd {t_fb*1e3:.3f} ms ({pairs/t_fb/1e9:.1f} Gpair/s)", flush=True)
+        print(f"{B}x{n}x{m}: fwd {t_f*1e3:.3f} ms ({pairs/t_f/1e9:.1f} Gpair/s; two-pass {pairs/t_2p/1e9:.1f})  fwd+bwd {t_fb*1e3:.3f} ms ({pairs/t_fb/1e9:.1f} Gpair/s)", flush=True)
     print(json.dumps(res))
 
 
