@@ -27,7 +27,7 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X fp32 (vector = matrix) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARY = "r1v_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
+PMC_SUMMARY = "r1x_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
 
 
 def workload_cfg(args):
@@ -233,6 +233,8 @@ def main():
                     help="run the source branch on a second stream (measured neutral: the GEMMs fill the GPU)")
     ap.add_argument("--all-slots", action="store_true",
                     help="encode every source slot (no unique-source encoding) in the timed run")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the chamfer / pseudo-label side measurements (step-only profiles)")
     ap.add_argument("--no-all-slots-rate", action="store_true",
                     help="skip the extra timed run that encodes every source slot")
     args = ap.parse_args()
@@ -384,10 +386,12 @@ def main():
     if all_slots_rate is not None:
         extra["all_slots_iters_s"] = round(all_slots_rate, 4)
     extra["unique_sources"] = bool(cfg["unique_sources"])
-    ch = chamfer_rate(dev)
-    extra["chamfer_gpair_s"] = ch["gpair_dist_s"]
-    extra["chamfer"] = [ch, chamfer_rate(dev, 64, 4096, 4096, iters=10), chamfer_rate(dev, 16, 16384, 2048, iters=10)]
-    extra["pseudo_label_dcd"] = pair_rate(dev)
+    if not args.no_extras:
+        ch = chamfer_rate(dev)
+        extra["chamfer_gpair_s"] = ch["gpair_dist_s"]
+        extra["chamfer"] = [ch, chamfer_rate(dev, 64, 4096, 4096, iters=10),
+                            chamfer_rate(dev, 16, 16384, 2048, iters=10)]
+        extra["pseudo_label_dcd"] = pair_rate(dev)
     extra["loss"] = loss_val
     cpu = None if args.no_cpu_baseline else cpu_baseline(args)
     out = {"metric": "train iters/sec chair bs=16 2048-pt @1/2/4/8 GPU; Chamfer Gpair-dist/s",
