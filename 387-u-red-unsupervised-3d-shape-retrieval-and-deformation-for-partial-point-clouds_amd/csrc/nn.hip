@@ -624,6 +624,47 @@ __global__ __launch_bounds__(DCD_THREADS) void dcd_kernel(const float* __restric
     }
 }
 
+// ---- per-part axis-aligned boxes (compute_aabbox, dataset/dataset_utils.py:77-85) ---------
+// One workgroup per segment of the label-sorted points: min / max of each coordinate (exact,
+// order-independent), then (center, half extent) = ((lo+hi)/2, (hi-lo)/2). Empty segments
+// give zeros, as the torch scatter_reduce(include_self=False) over a zero tensor did.
+__global__ __launch_bounds__(256) void seg_aabb_kernel(const float* __restrict__ x, const int* __restrict__ off,
+                                                       float* __restrict__ out) {
+    __shared__ float red[6][4];
+    const int g = blockIdx.x, t = threadIdx.x;
+    const int r0 = off[g], r1 = off[g + 1];
+    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+    for (int r = r0 + t; r < r1; r += 256) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float v = x[3 * (size_t)r + c];
+            lo[c] = fminf(lo[c], v);
+            hi[c] = fmaxf(hi[c], v);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            lo[c] = fminf(lo[c], __shfl_xor(lo[c], o));
+            hi[c] = fmaxf(hi[c], __shfl_xor(hi[c], o));
+        }
+    }
+    if ((t & 63) == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { red[c][t >> 6] = lo[c]; red[3 + c][t >> 6] = hi[c]; }
+    }
+    __syncthreads();
+    if (t < 3) {
+        const float l = fminf(fminf(red[t][0], red[t][1]), fminf(red[t][2], red[t][3]));
+        const float h = fmaxf(fmaxf(red[3 + t][0], red[3 + t][1]), fmaxf(red[3 + t][2], red[3 + t][3]));
+        const bool empty = r1 <= r0;
+        out[6 * (size_t)g + t] = empty ? 0.f : (l + h) / 2.0f;
+        out[6 * (size_t)g + 3 + t] = empty ? 0.f : (h - l) / 2.0f;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -732,6 +773,16 @@ int ured_nn_seg_bwd(const float* a, const float* b, const int* segs, int nseg,
     NNBwdArgs A{a, b, reinterpret_cast<const int4*>(segs), 0, 0, gd_a, gd_b, idx_a, idx_b, ga, gb};
     bwd_dispatch(A, nseg, max_a_len, max_b_len, (hipStream_t)stream);
     return ured::launch_status("ured_nn_seg_bwd");
+}
+
+int ured_seg_aabb(const float* x, const int* off, int G, float* out, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(G >= 0, "ured_seg_aabb: negative segment count");
+    if (G == 0) return 0;
+    URED_REQUIRE(x && off && out, "ured_seg_aabb: null pointer");
+    URED_REQUIRE(G <= (1 << 30), "ured_seg_aabb: too many segments");
+    hipLaunchKernelGGL(seg_aabb_kernel, dim3(G), dim3(256), 0, (hipStream_t)stream, x, off, out);
+    return ured::launch_status("ured_seg_aabb");
 }
 
 int ured_dcd(const float* dist1, const int* idx1, const float* dist2, const int* idx2, int b, int n1, int n2,

@@ -27,6 +27,7 @@ _SIGNATURES = {
     "ured_nn_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "ured_nn_seg_fwd": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_nn_fwd_workspace": [_I, _I, _I, _I, _I, _I],
+    "ured_seg_aabb": [_P, _P, _I, _P, _P],
     "ured_nn_fwd_ws": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _SZ, _P],
     "ured_nn_seg_fwd_ws": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _SZ, _P],
     "ured_nn_seg_bwd": [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],

@@ -11,6 +11,7 @@ build_parts   : computes a PartBatch with device ops only (no host sync).
 import torch
 from torch.autograd import Function
 
+from . import _lib
 from . import kernels as K
 
 
@@ -81,14 +82,18 @@ def build_parts(labels, x, max_parts):
 
 
 def part_aabb(parts):
-    """[B, P, 6] = (center, half extent) per part slot (compute_aabbox, dataset_utils.py:77-85)."""
+    """[B, P, 6] = (center, half extent) per part slot (compute_aabbox, dataset_utils.py:77-85):
+    one HIP segment min/max launch over the label-sorted points (ured_seg_aabb)."""
     B, N, _ = parts.x_sorted.shape
     P = parts.max_parts
-    idx = parts.gid.long().unsqueeze(1).expand(-1, 3)
     flat = parts.x_sorted.reshape(-1, 3)
-    lo = torch.zeros(B * P, 3, device=flat.device).scatter_reduce(0, idx, flat, "amin", include_self=False)
-    hi = torch.zeros(B * P, 3, device=flat.device).scatter_reduce(0, idx, flat, "amax", include_self=False)
-    return torch.cat([(lo + hi) / 2.0, (hi - lo) / 2.0], 1).view(B, P, 6)
+    if flat.dtype != torch.float32:
+        raise TypeError("part_aabb: float32 points expected")
+    _lib.require_device(flat)
+    flat = flat.contiguous()
+    out = torch.empty(B * P, 6, device=flat.device, dtype=torch.float32)
+    _lib.call("ured_seg_aabb", _lib.ptr(flat), _lib.ptr(parts.off), B * P, _lib.ptr(out), _lib.stream_of(flat))
+    return out.view(B, P, 6)
 
 
 class ExpandGroupsFn(Function):

@@ -193,6 +193,34 @@ def chamfer_rate(dev, B=16, n=2048, m=2048, iters=20):
             "hbm_read_frac": round(12 * B * (n + m) / t / 8e12, 6)}
 
 
+def inference_rate(cfg, db, dev, iters=10):
+    """Config 3 (table, bs=16, 2048 pts): the engine/test.py retrieval + deformation inference
+    path — encode the source DB once (eval BN, chunks of 512), then per batch: target encoder,
+    part pooling, cosine retrieval over the DB, DeformNet, get_shape, chamfer."""
+    from engine.test import encode_sources, infer
+    from engine.train import batch_to_device, get_models
+    from dataset import synthetic
+    models, _, _ = get_models(cfg, dev)
+    b = batch_to_device(synthetic.make_batch(16, 2048, db.num_sources, parts=4, seed=77), dev, db.num_sources)
+    codes = encode_sources(models, db)
+    infer(models, db, b, cfg, codes)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    codes = encode_sources(models, db)
+    torch.cuda.synchronize()
+    t_db = time.perf_counter() - t0
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        infer(models, db, b, cfg, codes)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / iters * 1e-3
+    return {"workload": "config 3: engine/test.py inference, bs=16, 2048 pts, 4 parts/target",
+            "batches_per_s": round(1.0 / t, 2), "targets_per_s": round(16.0 / t, 1), "ms_per_batch": round(t * 1e3, 3),
+            "source_db_encode_ms": round(t_db * 1e3, 3), "sources": int(db.num_sources)}
+
+
 def pair_rate(dev, parts=512, pts=1024):
     """§8f row 1: all-pairs calc_dcd pseudo-labels over `parts` source parts (upper triangle)."""
     from engine.generate_pair import PairGenerator, normalize_pts
@@ -392,6 +420,7 @@ def main():
         extra["chamfer"] = [ch, chamfer_rate(dev, 64, 4096, 4096, iters=10),
                             chamfer_rate(dev, 16, 16384, 2048, iters=10)]
         extra["pseudo_label_dcd"] = pair_rate(dev)
+        extra["inference"] = inference_rate(cfg, db, dev)
     extra["loss"] = loss_val
     cpu = None if args.no_cpu_baseline else cpu_baseline(args)
     out = {"metric": "train iters/sec chair bs=16 2048-pt @1/2/4/8 GPU; Chamfer Gpair-dist/s",

@@ -87,6 +87,11 @@ int ured_nn_seg_fwd_ws(const float* a, const float* b, const int* segs, int nseg
                        float* dist_a, int* idx_a, float* dist_b, int* idx_b,
                        void* workspace, size_t ws_bytes, void* stream);
 
+/* Per-part axis-aligned boxes (compute_aabbox, dataset/dataset_utils.py:77-85, as used by
+ * get_part, engine/train.py:119-128): x [R,3] points sorted by segment, off int32 [G+1] row
+ * offsets -> out [G,6] = (center, half extent) of each segment; empty segments give zeros. */
+int ured_seg_aabb(const float* x, const int* off, int G, float* out, void* stream);
+
 /* Backward of ured_nn_seg_fwd: accumulates into ga (a-points) and gb (b-points)
  * exactly the per-pair formula of ured_nn_bwd. gd_a / gd_b may be NULL. */
 int ured_nn_seg_bwd(const float* a, const float* b, const int* segs, int nseg,

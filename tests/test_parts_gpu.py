@@ -1,0 +1,38 @@
+"""Part bookkeeping on the device (engine/train.py:103-136 get_part helpers): the HIP
+segment AABB (ured_seg_aabb) vs compute_aabbox (dataset/dataset_utils.py:77-85) applied
+per part on the CPU — bit-exact (min / max are exact, then the same two fp32 ops)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _aabb_ref(v):
+    lo, hi = v.min(0).values, v.max(0).values
+    return torch.cat([(lo + hi) / 2.0, (hi - lo) / 2.0])
+
+
+@pytest.mark.parametrize("B,N,P,kmax", [(16, 2048, 16, 4), (3, 700, 16, 16), (2, 5, 8, 8)])
+def test_part_aabb_bitexact(dev, B, N, P, kmax):
+    from ured_hip.ops import build_parts, part_aabb
+    g = torch.Generator().manual_seed(B * N + P)
+    x = (torch.rand(B, N, 3, generator=g) * 2 - 1)
+    labels = torch.randint(0, kmax, (B, N), generator=g)
+    parts = build_parts(labels.to(dev), x.to(dev), P)
+    got = part_aabb(parts).cpu()
+    for b in range(B):
+        present = sorted(set(labels[b].tolist()))
+        for slot in range(P):
+            if slot < len(present):
+                exp = _aabb_ref(x[b][labels[b] == present[slot]])
+            else:
+                exp = torch.zeros(6)
+            assert torch.equal(got[b, slot], exp), (b, slot)
+
+
+def test_part_aabb_rejects_cpu():
+    from ured_hip.ops import PartBatch, part_aabb
+    pb = PartBatch(x_sorted=torch.zeros(1, 4, 3), off=torch.zeros(2, dtype=torch.int32), max_parts=1)
+    with pytest.raises(RuntimeError):
+        part_aabb(pb)

@@ -17,6 +17,7 @@ from torch.profiler import ProfilerActivity, profile  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--stacks", action="store_true", help="group the small ops by Python call stack")
     a = ap.parse_args()
     import bench
     from engine.dp import DataParallelStep
@@ -35,12 +36,22 @@ def main():
     for i in range(3):
         step.step(batches[i % 2])
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=False) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=False,
+                 with_stack=a.stacks) as prof:
         for i in range(a.steps):
             step.step(batches[i % 2])
         torch.cuda.synchronize()
     print(prof.key_averages().table(sort_by="self_device_time_total", row_limit=70, max_name_column_width=60))
     print(prof.key_averages(group_by_stack_n=0).table(sort_by="count", row_limit=40, max_name_column_width=60))
+    if a.stacks:
+        want = ("aten::add", "aten::add_", "aten::fill_", "aten::zero_", "aten::sum", "aten::copy_",
+                "aten::mul", "aten::cat", "aten::mm", "aten::addmm", "aten::bmm", "aten::div")
+        rows = [e for e in prof.key_averages(group_by_stack_n=6) if e.key in want]
+        rows.sort(key=lambda e: -e.device_time_total)
+        for e in rows[:60]:
+            print(f"{e.key:14s} n={e.count:4d} dev_us={e.device_time_total:9.1f}")
+            for fr in e.stack[:6]:
+                print("      ", fr)
 
 
 if __name__ == "__main__":
