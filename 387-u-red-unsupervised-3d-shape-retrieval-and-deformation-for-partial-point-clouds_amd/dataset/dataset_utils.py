@@ -5,8 +5,12 @@ get_shape       dataset_utils.py:691-726   A [B,P,3n,6] @ (weight*param + defaul
 get_source_info dataset_utils.py:791-820   (gathers from a device-resident SourceDB, no host copies)
 get_source_points dataset_utils.py:1008-1034
 get_symmetric   dataset_utils.py:1194-1196
-The rendering / mesh export / pickle-label helpers of that file are out of scope.
+get_shape_numpy dataset_utils.py:601-621    (+ deform_vertices: the same for every retrieved mesh at once)
+cal_retrieval_score dataset_utils.py:1165-1176 (+ ndcg_score: sklearn.metrics.ndcg_score on the device)
+The rendering / mesh export helpers of that file are out of scope; the pickle-label helpers
+(get_labels, mask_label) live in train_utils/pseudo_labels.py as a device table.
 """
+import numpy as np
 import torch
 
 
@@ -51,3 +55,74 @@ def get_source_info(source_labels, db, use_connectivity=False):
 
 def get_source_points(source_labels, db, device=None):
     return db.points[_index(source_labels, db)]
+
+
+def get_shape_numpy(A, param, src_default_param=None, weight=1.0, connectivity_mat=None):
+    """dataset_utils.py:601-621 (numpy, one part): A [3V, 6] @ (weight*param + default) -> [V, 3]."""
+    param = np.multiply(param, weight)
+    if src_default_param is not None:
+        param = param + src_default_param
+    if connectivity_mat is not None:
+        param = np.matmul(connectivity_mat, param)
+    return np.reshape(np.matmul(A, param), (-1, 3), order="C")
+
+
+def deform_vertices(vmats, voff, source_idx, params, default_params=None, weight=0.1):
+    """The vis.py:291-296 mesh step for every part slot of a batch at once: part slot (b, i) uses
+    the retrieved source's vertices_mat rows vmats[voff[s]:voff[s+1]] ([3V_s, 6], stacked for the
+    whole source DB) and p = weight*params[b,i] + default_params[b,i] (vis.py passes the target
+    part's AABB as the default). Returns (vertices [R, 3] flat over the slots in (b, i) order,
+    row offsets [B*P+1]) — a ragged GEMV, HBM-bound, as device ops without a host sync except the
+    output size (taken from the offsets' last entry)."""
+    B, P, pd = params.shape
+    src = source_idx.reshape(-1).long()
+    starts, ends = voff[src].long(), voff[src + 1].long()
+    counts = ends - starts                                             # rows (3 per vertex)
+    out_off = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0)])
+    total = int(out_off[-1])
+    slot = torch.repeat_interleave(torch.arange(B * P, device=params.device), counts, output_size=total)
+    row = starts[slot] + (torch.arange(total, device=params.device) - out_off[slot])
+    p = weight * params.reshape(B * P, pd)
+    if default_params is not None:
+        p = p + default_params.reshape(B * P, pd)
+    v = (vmats[row] * p[slot]).sum(-1)
+    return v.view(-1, 3), torch.div(out_off, 3, rounding_mode="floor")
+
+
+def ndcg_score(y_true, y_score, k=None):
+    """sklearn.metrics.ndcg_score (ignore_ties=False) for each row of [Q, L] float64 tensors:
+    tie-averaged DCG@k of y_true ranked by y_score over the ideal DCG@k; rows whose ideal DCG
+    is 0 score 0. Returns [Q] (sklearn's value for one row is the mean over a batch of one)."""
+    y_true = y_true.double()
+    y_score = y_score.double()
+    Q, L = y_true.shape
+    disc = 1.0 / torch.log2(torch.arange(L, device=y_true.device, dtype=torch.float64) + 2.0)
+    if k is not None:
+        disc[k:] = 0.0
+    s_sorted, order = torch.sort(y_score, dim=1, descending=True, stable=True)
+    rel = torch.gather(y_true, 1, order)
+    new = torch.ones_like(s_sorted, dtype=torch.bool)
+    new[:, 1:] = s_sorted[:, 1:] != s_sorted[:, :-1]
+    gid = torch.cumsum(new.long(), 1) - 1
+    gsum = torch.zeros_like(rel).scatter_add_(1, gid, rel)
+    gcnt = torch.zeros_like(rel).scatter_add_(1, gid, torch.ones_like(rel))
+    dcg = (torch.gather(gsum, 1, gid) / torch.gather(gcnt, 1, gid) * disc).sum(1)
+    ideal = torch.sort(y_true, dim=1, descending=True).values
+    idcg = (ideal * disc).sum(1)
+    return torch.where(idcg > 0, dcg / torch.where(idcg > 0, idcg, torch.ones_like(idcg)), torch.zeros_like(dcg))
+
+
+def cal_retrieval_score(y_score, cd_m, k=40, sigma=0.001, aligned=False):
+    """dataset_utils.py:1165-1176 for Q target parts at once: y_score [Q, NS] (cosine similarity
+    of each target part to every source), cd_m [Q, NS] (the part's pseudo-label row, what
+    read_pickle_topk reads) -> NDCG@k per part [Q].
+
+    The reference builds true_relevance = exp(-d^2 / (2 sigma^2)) from read_pickle_topk's
+    distances, which come back SORTED ascending (torch.topk(..., k=NS, largest=False)), and
+    scores them against y_score in source order; aligned=False reproduces that, aligned=True
+    scores each source's own relevance."""
+    d = cd_m.double()
+    if not aligned:
+        d = torch.sort(d, dim=1).values
+    rel = torch.exp(-d ** 2 / (2.0 * sigma ** 2))
+    return ndcg_score(rel, y_score.double(), k)

@@ -48,6 +48,26 @@ def make_source_db(num_sources, seed=1, np_per_part=NP_PER_PART):
     return {"src_points": pts, "src_mats": mats, "src_default_param": default_param, "src_sem": sem}
 
 
+def make_source_meshes(db, seed=2, vmin=100, vmax=600):
+    """Mesh side of the source DB (vertices / vertices_mat of run_preprocessing.py:852-862):
+    per source V_s vertices uniform in its AABB and vertices_mat rows [I3 | diag(q)] as for the
+    points. Stacked flat: vmats [sum 3V_s, 6] float32, voff int64 [NS+1] row offsets."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    c, s = db["src_default_param"][:, :3], db["src_default_param"][:, 3:]
+    mats, verts, off = [], [], [0]
+    for i in range(c.shape[0]):
+        V = int(rng.integers(vmin, vmax + 1))
+        q = rng.uniform(-1.0, 1.0, size=(V, 3)).astype(np.float32)
+        verts.append((c[i] + q * s[i]).astype(np.float32))
+        A = np.zeros((V, 3, 6), np.float32)
+        for r in range(3):
+            A[:, r, r] = 1.0
+            A[:, r, 3 + r] = q[:, r]
+        mats.append(A.reshape(3 * V, 6))
+        off.append(off[-1] + 3 * V)
+    return {"vertices": verts, "vmats": np.concatenate(mats), "voff": np.asarray(off, np.int64)}
+
+
 def make_batch(batch_size, num_points, num_sources, max_parts=16, parts=4, seed=0, invalid_frac=0.0):
     """One synthetic batch. `parts` is an int (k_b for every sample) or a list per sample."""
     rng = np.random.Generator(np.random.PCG64(seed))

@@ -61,15 +61,29 @@ class PairGenerator:
         self.n_lambda = n_lambda
         self.chunk = int(min(chunk_pairs, 65535))
 
-    def pairs(self, gi, xj):
-        """calc_dcd(x = points[xj], gt = points[gi]) for index vectors (device, int64) ->
-        (dcd, cd_s, cd_m) device tensors."""
+    def pairs(self, gi, xj, x_table=None):
+        """calc_dcd(x = x_table[xj], gt = points[gi]) for index vectors (device, int64) ->
+        (dcd, cd_s, cd_m) device tensors; x_table defaults to the resident table itself."""
+        xt = self.points if x_table is None else x_table
         outs = []
         for s in range(0, gi.numel(), self.chunk):
-            g, x = self.points[gi[s:s + self.chunk]], self.points[xj[s:s + self.chunk]]
+            g, x = self.points[gi[s:s + self.chunk]], xt[xj[s:s + self.chunk]]
             d1, d2, i1, i2 = unn.nn_dense(g, x)
             outs.append(torch.stack(unn.dcd(d1, i1, d2, i2, self.alpha, self.n_lambda)))
         return torch.cat(outs, 1) if outs else torch.empty(3, 0, device=self.points.device)
+
+    @torch.no_grad()
+    def cross(self, targets):
+        """Target parts x every resident source: calc_dcd(x = targets[t], gt = points[s]), the
+        per-target-part rows the training pseudo-labels are chosen from (the target branch of
+        get_data_pair, generate_pair.py:96-104: compute_dcd_loss(target part, source)).
+        targets [T, n, 3] (normalised like the sources) -> [3, T, NS] device (dcd, cd_s, cd_m)."""
+        targets = targets.to(self.points.device).contiguous().float()
+        T, NS = targets.shape[0], self.points.shape[0]
+        dev = self.points.device
+        gi = torch.arange(NS, device=dev).repeat(T)
+        xj = torch.arange(T, device=dev).repeat_interleave(NS)
+        return self.pairs(gi, xj, targets).view(3, T, NS)
 
     @torch.no_grad()
     def rows(self, rows):

@@ -9,6 +9,9 @@ working path is engine/vis.py:118-256, restated here batched and without host sy
   4. DeformNet on (target code, normalised retrieved codes) -> params; get_shape with the
      retrieved sources' A matrices and no default param (vis.py:243-252)
   5. chamfer of the deformed shape (all 16x1024 points, the unmasked branch vis.py:256 lands in)
+  6. (optional) the residual-net score max_points sum|r| (vis.py:221-231), NDCG@40 of the
+     retrieval scores against the pseudo-label rows (cal_retrieval_score, vis.py:207), and the
+     retrieved meshes deformed with the target parts' boxes as default (vis.py:278-296)
     python engine/test.py [config.json]
 """
 import json
@@ -23,7 +26,7 @@ if os.path.dirname(_HERE) not in sys.path:
     sys.path.insert(0, os.path.dirname(_HERE))
 
 from dataset import synthetic  # noqa: E402
-from dataset.dataset_utils import get_shape  # noqa: E402
+from dataset.dataset_utils import cal_retrieval_score, deform_vertices, get_shape  # noqa: E402
 from engine.train import batch_to_device, get_models, get_part  # noqa: E402
 from loss.chamfer_loss import compute_cm_loss  # noqa: E402
 from train_utils.load_sources import load_sources  # noqa: E402
@@ -43,9 +46,12 @@ def encode_sources(models, db, chunk=512):
 
 
 @torch.no_grad()
-def infer(models, db, batch, cfg, src_codes=None):
+def infer(models, db, batch, cfg, src_codes=None, relevance=None, meshes=None):
     """-> dict(retrieved [B,P] (-1 for empty slots), sim_top2_gap [B,P], params [B,P,6],
-    out [B,P*1024,3], cd [B] (chamfer_distance2 of out vs x))."""
+    out [B,P*1024,3], cd [B] (chamfer_distance2 of out vs x), re_score [B]) plus, with
+    `relevance` ([B,P,NS] pseudo-label cd_m rows of the target parts), ndcg [B,P] (NaN for empty
+    slots), and with `meshes` ({"vmats","voff"} device tensors of the source DB), the deformed
+    retrieved meshes (vertices [R,3], vertex offsets [B*P+1])."""
     for m in models.values():
         m.eval()
     if src_codes is None:
@@ -54,7 +60,7 @@ def infer(models, db, batch, cfg, src_codes=None):
     B, N, _ = x.shape
     P = cfg["MAX_NUM_PARTS"]
     tcode, pp = models["target_encoder_full"].forward_pointmajor(x, models["embedding_layer"](batch["tgt_sem"]))
-    part_f, _, _, mask, _, _ = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
+    part_f, _, re_in, mask, _, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
     part_n = F.normalize(part_f, dim=-1, p=2)
     sim = part_n @ src_codes.t()                                      # [B, P, NS]
     top2 = sim.topk(2, dim=-1).values
@@ -64,8 +70,17 @@ def infer(models, db, batch, cfg, src_codes=None):
     params = models["param_decoder_full"](tcode, src_codes[idx], None)
     out = get_shape(db.mats[idx], params, None, cfg["alpha"]).reshape(B, -1, 3)
     cd = compute_cm_loss(out, x, mask, batch_reduction=None)          # unmasked branch, like vis.py:256
-    return {"retrieved": retrieved, "sim_top2_gap": top2[..., 0] - top2[..., 1], "params": params,
-            "out": out, "cd": cd, "mask": mask}
+    res = models["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
+                                                        off=re_in.off).view(B, N, 3)
+    r = {"retrieved": retrieved, "sim_top2_gap": top2[..., 0] - top2[..., 1], "params": params,
+         "out": out, "cd": cd, "mask": mask, "re_score": res.abs().sum(-1).amax(-1)}
+    if relevance is not None:
+        nd = cal_retrieval_score(sim.reshape(B * P, -1), relevance.reshape(B * P, -1)).view(B, P)
+        r["ndcg"] = torch.where(mask > 0, nd, torch.full_like(nd, float("nan")))
+    if meshes is not None:
+        r["vertices"], r["vertex_off"] = deform_vertices(meshes["vmats"], meshes["voff"], idx, params,
+                                                         param_def, cfg["alpha"])
+    return r
 
 
 def main(cfg):

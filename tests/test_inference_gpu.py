@@ -44,3 +44,53 @@ def test_inference_matches_oracle(dev):
     cd, rcd = r["cd"].cpu(), R["cd"]
     np.testing.assert_allclose(cd[same].numpy(), rcd[same].numpy(), rtol=1e-4)
     np.testing.assert_allclose(r["params"].cpu()[same].numpy(), R["params"][same].numpy(), rtol=1e-3, atol=1e-5)
+
+
+def test_inference_scores_and_meshes(dev):
+    """vis.py's per-batch extras: residual score max_pts sum|r| (vis.py:221-231), NDCG@40 per
+    target part (cal_retrieval_score, vs sklearn in tests/test_retrieval_metrics.py), and the
+    retrieved meshes deformed with the target-part boxes (get_shape_numpy per part)."""
+    from sklearn.metrics import ndcg_score as sk_ndcg
+    from dataset import synthetic
+    from dataset.dataset_utils import get_shape_numpy
+    from train_utils.load_sources import SourceDB
+    from engine.train import get_models, batch_to_device, get_part
+    from engine.test import encode_sources, infer
+    import torch.nn.functional as F
+    ns = 300
+    dbn = synthetic.make_source_db(ns, seed=21)
+    mesh = synthetic.make_source_meshes(dbn, seed=22, vmin=10, vmax=60)
+    bt = synthetic.make_batch(2, 256, ns, parts=[3, 5], seed=23)
+    db = SourceDB(dbn["src_points"], dbn["src_mats"], dbn["src_default_param"], dbn["src_sem"], dev)
+    models, _, _ = get_models(CFG, dev)
+    b = batch_to_device(bt, dev)
+    rng = np.random.Generator(np.random.PCG64(24))
+    rel = torch.from_numpy(rng.uniform(0, 0.004, size=(2, 16, ns))).to(dev)
+    meshes = {"vmats": torch.from_numpy(mesh["vmats"]).to(dev), "voff": torch.from_numpy(mesh["voff"]).to(dev)}
+    codes = encode_sources(models, db)
+    r = infer(models, db, b, CFG, codes, relevance=rel, meshes=meshes)
+    # NDCG: the same similarity rows scored by sklearn
+    with torch.no_grad():
+        tcode, pp = models["target_encoder_full"].forward_pointmajor(b["x"], models["embedding_layer"](b["tgt_sem"]))
+        part_f, _, _, mask, _, param_def = get_part(CFG, pp.view(2, 256, -1), b["labels"], b["x"])
+        sim = (F.normalize(part_f, dim=-1, p=2) @ codes.t()).double().cpu().numpy()
+    nd = r["ndcg"].cpu().numpy()
+    for bb, k in enumerate((3, 5)):
+        for i in range(16):
+            if i >= k:
+                assert np.isnan(nd[bb, i])
+                continue
+            true = np.exp(-np.sort(rel[bb, i].cpu().numpy()) ** 2 / (2.0 * 0.001 ** 2))
+            assert abs(nd[bb, i] - sk_ndcg([true.tolist()], [sim[bb, i].tolist()], k=40)) < 1e-9
+    assert r["re_score"].shape == (2,) and bool(torch.isfinite(r["re_score"]).all())
+    # meshes
+    v, off = r["vertices"].cpu().numpy(), r["vertex_off"].cpu().numpy()
+    idx = r["retrieved"].cpu().numpy()
+    idx = np.where(idx < 0, idx + ns, idx)
+    params, pdef = r["params"].cpu().numpy(), param_def.cpu().numpy()
+    for bb in range(2):
+        for i in range(16):
+            s = idx[bb, i]
+            A = mesh["vmats"][mesh["voff"][s]:mesh["voff"][s + 1]]
+            exp = get_shape_numpy(A, params[bb, i].reshape(1, 6, 1), pdef[bb, i].reshape(6, 1), 0.1).reshape(-1, 3)
+            np.testing.assert_allclose(v[off[bb * 16 + i]:off[bb * 16 + i + 1]], exp, rtol=1e-5, atol=1e-6)
