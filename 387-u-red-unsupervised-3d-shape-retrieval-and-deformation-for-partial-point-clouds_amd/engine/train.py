@@ -117,6 +117,8 @@ class TrainStep:
         dev = torch.device(device or cfg["device"])
         self.side_stream = (torch.cuda.Stream(device=dev)
                             if dev.type == "cuda" and cfg.get("stream_overlap", False) else None)
+        self.deform_stream = (torch.cuda.Stream(device=dev)
+                              if dev.type == "cuda" and cfg.get("deform_overlap", False) else None)
 
     def _source_branch(self, uq, src_points, src_sem_f, B, P):
         """src_encoder_all + recon_decoder_src (engine/train.py:210-216) -> codes [B*P, C],
@@ -138,6 +140,29 @@ class TrainStep:
         recon_src_p = M["recon_decoder_src"].forward_split(src_pp, codes, code_first=True,
                                                            group_rows=self.np_per_part).view(B, P, -1, 3)
         return codes, recon_src_p
+
+    def _deform_losses(self, T, tcode, codes, mats, param_def, x, part_x, mask_part, target_part_f, src_labels):
+        """param_decoder_full -> get_shape -> chamfer (full, part), contrast and symmetry terms
+        (engine/train.py:253-302) -> (their weighted sum, out, params)."""
+        cfg, M = self.cfg, self.models
+        B = x.shape[0]
+        params_full = M["param_decoder_full"](tcode, codes, None)
+        out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
+        contrast_labels = torch.where(src_labels >= 0, torch.ones_like(src_labels), src_labels)
+        loss = out.new_zeros(())
+        if cfg["use_chamfer_loss"] > 0.0:
+            T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask_part,
+                                                                   np_per_part=self.np_per_part)
+            loss = loss + T["cd_loss_full"] * cfg["use_chamfer_loss"] + T["cd_loss_part"] * cfg["use_chamfer_part_loss"]
+        if cfg["use_contrast_loss"] > 0.0:
+            T["contrast_loss"] = compute_contrast_loss_loss(target_part_f, codes, contrast_labels,
+                                                            cfg.get("differentiable_gather", False))
+            loss = loss + T["contrast_loss"] * cfg["use_contrast_loss"]
+        if cfg["use_symmetry_loss"] > 0.0:
+            T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(get_symmetric(out), x, part_x, mask_part,
+                                                                           np_per_part=self.np_per_part)
+            loss = loss + T["ref_cd_loss_full"] * cfg["use_symmetry_loss"]
+        return loss, out, params_full
 
     def forward(self, batch, epoch=0):
         cfg, M = self.cfg, self.models
@@ -167,32 +192,39 @@ class TrainStep:
             codes, recon_src_p = self._source_branch(uq, src_points, src_sem_f, B, P)
         tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
         target_part_f, _, re_in, mask_part, part_x, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
-        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
-        re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
-                                                         off=re_in.off).view(B, N, 3)
         if side is not None:
             main.wait_stream(side)
             codes.record_stream(main)
             recon_src_p.record_stream(main)
         codes = codes.view(B, P, -1)
-        params_full = M["param_decoder_full"](tcode, codes, None)
-        out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
-        contrast_labels = torch.where(src_labels >= 0, torch.ones_like(src_labels), src_labels)
-
         T = {}
-        loss = out.new_zeros(())
-        if cfg["use_chamfer_loss"] > 0.0:
-            T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask_part,
-                                                                   np_per_part=self.np_per_part)
-            loss = loss + T["cd_loss_full"] * cfg["use_chamfer_loss"] + T["cd_loss_part"] * cfg["use_chamfer_part_loss"]
-        if cfg["use_contrast_loss"] > 0.0:
-            T["contrast_loss"] = compute_contrast_loss_loss(target_part_f, codes, contrast_labels,
-                                                            cfg.get("differentiable_gather", False))
-            loss = loss + T["contrast_loss"] * cfg["use_contrast_loss"]
-        if cfg["use_symmetry_loss"] > 0.0:
-            T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(get_symmetric(out), x, part_x, mask_part,
-                                                                           np_per_part=self.np_per_part)
-            loss = loss + T["ref_cd_loss_full"] * cfg["use_symmetry_loss"]
+        dside = self.deform_stream
+        if dside is not None:
+            # DeformNet + get_shape + the chamfer / contrast / symmetry losses are hundreds of
+            # latency-bound small kernels; on their own stream they (and, autograd running each
+            # node on its forward stream, their backward) overlap the GEMM-bound residual and
+            # reconstruction nets of the main stream
+            main = torch.cuda.current_stream(x.device)
+            dside.wait_stream(main)
+            for t in (tcode, codes, mats, param_def, x, target_part_f, mask_part, src_labels):
+                t.record_stream(dside)
+            for t in vars(part_x).values():
+                if torch.is_tensor(t):
+                    t.record_stream(dside)
+            with torch.cuda.stream(dside):
+                loss_d, out, params_full = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
+                                                               mask_part, target_part_f, src_labels)
+        else:
+            loss_d, out, params_full = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
+                                                           mask_part, target_part_f, src_labels)
+        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
+        re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
+                                                         off=re_in.off).view(B, N, 3)
+        if dside is not None:
+            main.wait_stream(dside)
+            for t in [loss_d, out, params_full] + [v for v in T.values() if torch.is_tensor(v)]:
+                t.record_stream(main)
+        loss = loss_d
         if cfg["use_residuals_reg"] > 0.0 and epoch > cfg["init_p_m_loss"]:
             T["re_reg_loss_full"], T["reg_loss_full"] = residual_retrieval_loss(x, out.detach(), re_res, mask_part,
                                                                                 np_per_part=self.np_per_part)
@@ -206,9 +238,31 @@ class TrainStep:
         T["_params"] = params_full
         return loss, T
 
-    def clip_and_step(self):
-        for name in CLIPPED:
-            torch.nn.utils.clip_grad_norm_(self.models[name].parameters(), 5.0)
+    def clip_and_step(self, max_norm=5.0):
+        """clip_grad_norm_(module.parameters(), 5.0) for each of the six modules
+        (engine/train.py:331-336) with the per-tensor norms of all six in one multi-tensor
+        launch and the six totals / clip factors as one small vector (deterministic: fixed-order
+        row sums, no atomics); then Adam."""
+        groups = [[p.grad for p in self.models[name].parameters() if p.grad is not None] for name in CLIPPED]
+        grads = [g for grp in groups for g in grp]
+        if grads:
+            counts = tuple(len(grp) for grp in groups)
+            key = (counts, grads[0].device)
+            if getattr(self, "_clip_key", None) != key:
+                L, n = max(counts), len(grads)
+                idx = torch.full((len(counts), L), n, dtype=torch.long)
+                o = 0
+                for g, c in enumerate(counts):
+                    idx[g, :c] = torch.arange(o, o + c)
+                    o += c
+                self._clip_idx, self._clip_key = idx.to(grads[0].device), key
+            norms = torch.stack(torch._foreach_norm(grads, 2.0))
+            sq = torch.cat([norms * norms, norms.new_zeros(1)])
+            total = sq[self._clip_idx].sum(1).sqrt()                       # [6] module norms
+            coef = (max_norm / (total + 1e-6)).clamp(max=1.0)
+            for g, grp in enumerate(groups):
+                if grp:
+                    torch._foreach_mul_(grp, coef[g])
         self.optimizer.step()
 
     def step(self, batch, epoch=0):

@@ -261,6 +261,8 @@ def main():
                     help="run the source branch on a second stream (measured neutral: the GEMMs fill the GPU)")
     ap.add_argument("--all-slots", action="store_true",
                     help="encode every source slot (no unique-source encoding) in the timed run")
+    ap.add_argument("--deform-overlap", action="store_true",
+                    help="DeformNet + chamfer/contrast losses on a side stream (overlaps the residual nets)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the chamfer / pseudo-label side measurements (step-only profiles)")
     ap.add_argument("--no-all-slots-rate", action="store_true",
@@ -286,6 +288,7 @@ def main():
     use_graph = args.graph and (world == 1 or args.graph_dp)
     cfg["cuda_graph"] = use_graph
     cfg["stream_overlap"] = args.overlap
+    cfg["deform_overlap"] = args.deform_overlap
     db, _ = load_sources(cfg, dev)
     eager = DataParallelStep(cfg, db, dev)
     cfg["unique_sources"] = not args.all_slots

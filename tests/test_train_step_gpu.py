@@ -145,3 +145,25 @@ def test_unique_sources_equal_all_slots(dev):
                 assert torch.allclose(v, b2s[k], rtol=1e-4, atol=1e-6), f"{name}.{k}"
             else:
                 assert torch.equal(v, b2s[k])
+
+
+def test_fused_clip_matches_clip_grad_norm(dev):
+    """TrainStep.clip_and_step's one-launch clipping == torch.nn.utils.clip_grad_norm_ per module
+    (engine/train.py:331-336) up to fp32 rounding of the six module norms."""
+    from engine.train import CLIPPED
+    ts = _setup(dev)[0]
+    for name in CLIPPED:                      # large gradients so that every module is clipped
+        for p in ts.models[name].parameters():
+            p.grad = torch.randn_like(p) * 10.0
+    ref = {name: [p.grad.clone() for p in ts.models[name].parameters()] for name in CLIPPED}
+    for name in CLIPPED:
+        gs = ref[name]                        # clip_grad_norm_'s arithmetic on the copies
+        total = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g) for g in gs]))
+        coef = (5.0 / (total + 1e-6)).clamp(max=1.0)
+        for g in gs:
+            g.mul_(coef)
+    ts.optimizer.step = lambda: None          # clip only
+    ts.clip_and_step()
+    for name in CLIPPED:
+        for p, r in zip(ts.models[name].parameters(), ref[name]):
+            torch.testing.assert_close(p.grad, r, rtol=2e-6, atol=1e-9)
