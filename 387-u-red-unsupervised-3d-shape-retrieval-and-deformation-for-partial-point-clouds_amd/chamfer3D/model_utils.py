@@ -1,4 +1,4 @@
-"""Drop-in for calc_cd / calc_dcd / fscore (Density_aware_Chamfer_Distance/utils_v2/model_utils.py:13-70,
+"""Drop-in for calc_cd / calc_dcd / calc_emd / fscore (Density_aware_Chamfer_Distance/utils_v2/model_utils.py:13-76,
 utils_v2/metrics/CD/fscore.py) on the HIP nearest-neighbour kernels.
 
 Note the reference's argument order: calc_cd(output, gt) evaluates cham_loss(gt, output), so
@@ -64,3 +64,11 @@ def calc_dcd(x, gt, alpha=1000, n_lambda=1, return_raw=False, non_reg=False):
     if return_raw:
         res.extend([dist1, dist2, idx1, idx2])
     return res
+
+
+def calc_emd(output, gt, eps=0.005, iterations=50):
+    """utils_v2/model_utils.py:72-76: auction EMD (emdModule on csrc/emd.hip) ->
+    (sqrt(dist).mean(1) [B], dist [B, n])."""
+    from emd import emd
+    dist, _ = emd()(output, gt, eps, iterations)
+    return torch.sqrt(dist).mean(1), dist

@@ -28,6 +28,9 @@ _SIGNATURES = {
     "ured_nn_seg_fwd": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_nn_fwd_workspace": [_I, _I, _I, _I, _I, _I],
     "ured_seg_aabb": [_P, _P, _I, _P, _P],
+    "ured_emd_workspace": [_I, _I],
+    "ured_emd_fwd": [_P, _P, _I, _I, _F, _I, _P, _P, _P, _SZ, _P],
+    "ured_emd_bwd": [_P, _P, _I, _I, _P, _P, _P, _P],
     "ured_nn_fwd_ws": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _SZ, _P],
     "ured_nn_seg_fwd_ws": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _SZ, _P],
     "ured_nn_seg_bwd": [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
@@ -35,7 +38,7 @@ _SIGNATURES = {
 }
 
 # entry points that return a value instead of a status (see query())
-_RESTYPES = {"ured_nn_fwd_workspace": _SZ}
+_RESTYPES = {"ured_nn_fwd_workspace": _SZ, "ured_emd_workspace": _SZ}
 
 _lib = None
 

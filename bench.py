@@ -193,6 +193,29 @@ def chamfer_rate(dev, B=16, n=2048, m=2048, iters=20):
             "hbm_read_frac": round(12 * B * (n + m) / t / 8e12, 6)}
 
 
+def emd_rate(dev, B=16, n=2048, eps=0.005, iters=50, reps=5):
+    """§8(f)4: calc_emd's default auction (eps 0.005, 50 rounds, utils_v2/model_utils.py:72) on
+    16 x 2048-point clouds: ms per call and the fraction of points matched one-to-one."""
+    from emd import emd
+    g = torch.Generator().manual_seed(0)
+    x1 = torch.rand(B, n, 3, generator=g).to(dev)
+    x2 = torch.rand(B, n, 3, generator=g).to(dev)
+    m = emd()
+    m(x1, x2, eps, iters)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dist, asg = m(x1, x2, eps, iters)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps
+    uniq = sum(int(torch.unique(asg[b]).numel()) for b in range(B)) / (B * n)
+    return {"shape": f"{B}x{n}", "eps": eps, "rounds": iters, "ms": round(t, 3),
+            "ms_per_round": round(t / max(iters, 1), 4),
+            "bijective_fraction": round(uniq, 4), "emd": round(float(torch.sqrt(dist).mean()), 6)}
+
+
 def inference_rate(cfg, db, dev, iters=10):
     """Config 3 (table, bs=16, 2048 pts): the engine/test.py retrieval + deformation inference
     path — encode the source DB once (eval BN, chunks of 512), then per batch: target encoder,
@@ -424,6 +447,7 @@ def main():
                             chamfer_rate(dev, 16, 16384, 2048, iters=10)]
         extra["pseudo_label_dcd"] = pair_rate(dev)
         extra["inference"] = inference_rate(cfg, db, dev)
+        extra["emd"] = emd_rate(dev)
     extra["loss"] = loss_val
     cpu = None if args.no_cpu_baseline else cpu_baseline(args)
     out = {"metric": "train iters/sec chair bs=16 2048-pt @1/2/4/8 GPU; Chamfer Gpair-dist/s",

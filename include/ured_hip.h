@@ -21,6 +21,7 @@
  *                       loss/basic_loss.py:249-265 (pytorch3d knn_points K=1),
  *                       batched into one ragged launch.
  *   ured_nn_fwd_ws / ured_nn_seg_fwd_ws <- the same two, both directions in one pass
+ *   ured_emd_fwd / ured_emd_bwd <- emd.forward / emd.backward (utils_v2/metrics/EMD/emd.cpp:14-24)
  *   ured_nn_seg_bwd  <- autograd of the above (NmDistanceGradKernel semantics,
  *                       chamfer3D.cu:155-174, made deterministic).
  */
@@ -91,6 +92,20 @@ int ured_nn_seg_fwd_ws(const float* a, const float* b, const int* segs, int nseg
  * get_part, engine/train.py:119-128): x [R,3] points sorted by segment, off int32 [G+1] row
  * offsets -> out [G,6] = (center, half extent) of each segment; empty segments give zeros. */
 int ured_seg_aabb(const float* x, const int* off, int G, float* out, void* stream);
+
+/* ---------------- EMD (auction algorithm) ---------------- */
+/* Approximate EMD matching of xyz1 [b,n,3] to xyz2 [b,n,3] (reference emd.forward,
+ * utils_v2/metrics/EMD/emd.cpp:14-19 -> emd_cuda.cu:183-256): `iters` auction rounds with
+ * parameter eps; assignment[b,n] = matched xyz2 index, dist[b,n] = squared distance to it.
+ * Deterministic (highest increment wins an object, ties to the lowest bidder index; scan ties to
+ * the lowest object index). Workspace: ured_emd_workspace(b, n) bytes, no initialisation. */
+size_t ured_emd_workspace(int b, int n);
+int ured_emd_fwd(const float* xyz1, const float* xyz2, int b, int n, float eps, int iters,
+                 float* dist, int* assignment, void* workspace, size_t ws_bytes, void* stream);
+/* gradxyz1 += 2 graddist (xyz1 - xyz2[assignment]) (reference emd.backward, emd_cuda.cu:283-304;
+ * xyz2 gets no gradient, as in emd_module.py:76-80). */
+int ured_emd_bwd(const float* xyz1, const float* xyz2, int b, int n, const float* graddist, const int* assignment,
+                 float* gradxyz1, void* stream);
 
 /* Backward of ured_nn_seg_fwd: accumulates into ga (a-points) and gb (b-points)
  * exactly the per-pair formula of ured_nn_bwd. gd_a / gd_b may be NULL. */
