@@ -300,7 +300,13 @@ int fwd_dispatch(const NNFwdArgs& a, int nseg, int max_a, int max_b, hipStream_t
 // or query group (QPT queries) for the first index with d == min: the reference's
 // lowest-index tie rule, exactly, with every distance evaluated by the contract formula.
 constexpr int NF_TILE = 512;    // refs per LDS fill (per wave, 6 KiB SoA)
-constexpr int NF_TARGET_WAVES = 4096;
+#ifndef URED_NF_TARGET_WAVES
+#define URED_NF_TARGET_WAVES 4096
+#endif
+#ifndef URED_NF_QPT16_PAIRS
+#define URED_NF_QPT16_PAIRS (1ll << 28)
+#endif
+constexpr int NF_TARGET_WAVES = URED_NF_TARGET_WAVES;
 
 struct NNFusedArgs {
     const float* a; const float* b; const int4* segs;
@@ -354,13 +360,9 @@ __device__ __forceinline__ void wave_min4(unsigned (&v)[4], unsigned (&w)[4]) {
     }
 }
 
-// v_writelane_b32: lane `sel` of dst := src (both scalar); no builtin in this toolchain. The
-// lane select goes through m0 (one SGPR operand per VALU instruction: constant-bus limit),
-// with one wait state after the m0 write.
-__device__ __forceinline__ unsigned writelane(unsigned dst, unsigned src, int sel) {
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0" : "+v"(dst) : "s"(src), "s"(sel) : "m0");
-    return dst;
-}
+// v_writelane_b32 (lane `sel` of `old` := src, both wave-uniform): the LLVM intrinsic under its
+// IR name (this toolchain has no clang builtin for it); the compiler routes `sel` through m0.
+__device__ int ured_writelane(int src, int sel, int old) __asm("llvm.amdgcn.writelane.i32");
 
 template <int QPT>
 __global__ __launch_bounds__(64) void nn_fused_kernel(NNFusedArgs A) {
@@ -416,7 +418,7 @@ __global__ __launch_bounds__(64) void nn_fused_kernel(NNFusedArgs A) {
             float mn[QPT];
 #pragma unroll
             for (int i = 0; i < QPT; ++i) mn[i] = __builtin_inff();
-            unsigned klo = 0, khi = 0;   // lane k < 16: column key of ref k of this chunk
+            int klo = 0, khi = 0;        // lane k < 16: column key (tag, value bits) of ref k of this chunk
 #pragma unroll 1
             for (int p = 0; p < 16; p += 4) {
                 f2 rx[4], ry[4], rz[4];
@@ -448,8 +450,8 @@ __global__ __launch_bounds__(64) void nn_fused_kernel(NNFusedArgs A) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const unsigned tag = (unsigned)qgroup0 + (unsigned)__builtin_ctzll(__ballot(v[k] == w[k]));
-                    klo = writelane(klo, tag, p + k);
-                    khi = writelane(khi, w[k], p + k);
+                    klo = ured_writelane((int)tag, p + k, klo);
+                    khi = ured_writelane((int)w[k], p + k, khi);
                 }
             }
             const int gc = (t0 + c * 16) >> 4;       // chunk index within the segment's refs
@@ -458,7 +460,7 @@ __global__ __launch_bounds__(64) void nn_fused_kernel(NNFusedArgs A) {
                 if (mn[i] < best[i]) { best[i] = mn[i]; bchunk[i] = gc; }
             const int r = t0 + c * 16 + lane;
             if (lane < 16 && r < r_end)
-                colslab[r] = ((unsigned long long)khi << 32) | klo;
+                colslab[r] = ((unsigned long long)(unsigned)khi << 32) | (unsigned)klo;
         }
     }
     unsigned long long* rowslab = A.rowslab + (size_t)rs * A.a_total + ao;
@@ -524,7 +526,7 @@ FusedPlan fused_plan(int nseg, int max_a, int max_b, int a_total, int b_total) {
     FusedPlan p{};
     if (nseg <= 0 || max_a <= 0 || max_b <= 0) return p;
     const long long pairs = (long long)nseg * max_a * max_b;
-    p.qpt = (pairs >= (1ll << 28) && max_a >= 1024) ? 16 : 8;
+    p.qpt = (pairs >= URED_NF_QPT16_PAIRS && max_a >= 1024) ? 16 : 8;
     const int qtile = 64 * p.qpt;
     p.qtiles = (max_a + qtile - 1) / qtile;
     const long long base = (long long)nseg * p.qtiles;
