@@ -74,6 +74,37 @@ class ResidualAttentionMessagePropagation(nn.Module):
         first = xq - message if self.use_offset else xq
         return xq + self.fc.forward_nodes(torch.cat([first, message], dim=-1))
 
+    def forward_nodes_self_pair(self, x0, x1):
+        """(forward_nodes(x0), forward_nodes(x1)) — the two self-attention calls of a
+        DescriptorsSelfAttention layer (shared weights) — with every linear layer run once over
+        the rows of both node sets: the attention and each BatchNorm still see one set at a
+        time (same batch statistics, same running-stat update order), so the values are those
+        of the two calls; half the GEMM launches, no gradient accumulation across the calls."""
+        fc = self.fc
+        mha = self.mha
+        if mha.attention_func is not softmax_attention or fc.use_norm not in ("use_bn", "None", None):
+            return self.forward_nodes(x0), self.forward_nodes(x1)
+        B, n0, C = x0.shape
+        n1 = x1.shape[1]
+        R0 = B * n0
+        X = torch.cat([x0.reshape(R0, C), x1.reshape(B * n1, C)])
+        q_, k_, v_ = mha.in_proj_q, mha.in_proj_k, mha.in_proj_v
+        qkv = F.linear(X, torch.cat([mha._w(q_), mha._w(k_), mha._w(v_)]), torch.cat([q_.bias, k_.bias, v_.bias]))
+        o = torch.cat([self_attention(qkv[:R0].view(B, n0, -1), mha.num_heads).reshape(R0, C),
+                       self_attention(qkv[R0:].view(B, n1, -1), mha.num_heads).reshape(B * n1, C)])
+        message = F.linear(o, mha._w(mha.out_proj), mha.out_proj.bias)
+        first = X - message if self.use_offset else X
+        h = torch.cat([first, message], dim=-1)
+        for layer in fc:
+            if isinstance(layer, nn.Conv1d):
+                h = F.linear(h, layer.weight.view(layer.weight.shape[0], -1), layer.bias)
+            elif isinstance(layer, nn.ReLU):
+                h = F.relu(h)
+            else:                                          # BatchNorm1d: one node set at a time
+                h = torch.cat([layer(h[:R0]), layer(h[R0:])])
+        out = X + h
+        return out[:R0].view(B, n0, C), out[R0:].view(B, n1, C)
+
 
 class DescriptorsSelfAttention(nn.Module):
     def __init__(self, embed_dim, num_heads, attention="softmax", use_offset=False):
@@ -84,7 +115,7 @@ class DescriptorsSelfAttention(nn.Module):
         return self.module(desc0, desc0), self.module(desc1, desc1)
 
     def forward_nodes(self, desc0, desc1):
-        return self.module.forward_nodes(desc0), self.module.forward_nodes(desc1)
+        return self.module.forward_nodes_self_pair(desc0, desc1)
 
 
 class DescriptorsCrossAttention(nn.Module):

@@ -286,6 +286,8 @@ def main():
                     help="encode every source slot (no unique-source encoding) in the timed run")
     ap.add_argument("--deform-overlap", action="store_true",
                     help="DeformNet + chamfer/contrast losses on a side stream (overlaps the residual nets)")
+    ap.add_argument("--blas", choices=["default", "hipblaslt", "rocblas"], default="rocblas",
+                    help="torch matmul backend for the small DeformNet / contrast GEMMs")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the chamfer / pseudo-label side measurements (step-only profiles)")
     ap.add_argument("--no-all-slots-rate", action="store_true",
@@ -302,6 +304,8 @@ def main():
     torch.manual_seed(1234 + rank)
 
     ge.build()
+    if args.blas != "default":
+        torch.backends.cuda.preferred_blas_library("cublaslt" if args.blas == "hipblaslt" else "cublas")
     from engine.dp import DataParallelStep
     from engine.train import batch_to_device
     from train_utils.load_sources import load_sources

@@ -85,35 +85,52 @@ def _channel_first_forward(net, target_f, src_part_f):
     return net.param_decoder(torch.cat([gr, pa], dim=1)).permute(0, 2, 1).contiguous()
 
 
+def _err(a, b):
+    return (a.detach().double().cpu() - b.detach().double().cpu()).abs().max().item()
+
+
 @pytest.mark.parametrize("C", [64, 512])
 def test_deformnet_node_major_equals_channel_first(dev, C):
+    """Node-major DeformNet (fused q|k|v, HIP attention, the two self-attention calls of a layer
+    batched into one set of GEMMs) vs the reference's channel-first forward: both fp32 runs are
+    compared with the same forward in float64; ours must stay as close to it as the fp32
+    reference-layout run is (BatchNorm over 32-row node sets amplifies GEMM rounding, so the two
+    fp32 runs differ from each other by more than either differs from float64)."""
     import copy
     from network.deformation_net import DeformNet_MatchingNet
     torch.manual_seed(C)
     net = DeformNet_MatchingNet(3 * C, graph_dim=C, max_num_parts=16, matching=False).to(dev).train()
     ref = copy.deepcopy(net)
+    ref64 = copy.deepcopy(net).double()
     tf = torch.randn(16, C, device=dev)
     sp = torch.randn(16, 16, C, device=dev)
     a_t, a_s = tf.clone().requires_grad_(True), sp.clone().requires_grad_(True)
     b_t, b_s = tf.clone().requires_grad_(True), sp.clone().requires_grad_(True)
+    c_t, c_s = tf.double().requires_grad_(True), sp.double().requires_grad_(True)
     out = net(a_t, a_s, None)
     rout = _channel_first_forward(ref, b_t, b_s)
+    tout = _channel_first_forward(ref64, c_t, c_s)
     assert out.shape == (16, 16, 6)
-    _close(out, rout, 1e-4)
     go = torch.randn_like(out)
     out.backward(go)
     rout.backward(go)
-    _close(a_t.grad, b_t.grad, 1e-4)
-    _close(a_s.grad, b_s.grad, 1e-4)
-    rp = dict(ref.named_parameters())
+    tout.backward(go.double())
+
+    def check(x, r, t, what):
+        e_ours, e_ref = _err(x, t), _err(r, t)
+        assert e_ours <= 3.0 * e_ref + 1e-5 * t.detach().abs().max().item() + 1e-9, (what, e_ours, e_ref)
+    check(out, rout, tout, "out")
+    check(a_t.grad, b_t.grad, c_t.grad, "target_f grad")
+    check(a_s.grad, b_s.grad, c_s.grad, "src_part_f grad")
+    rp, tp = dict(ref.named_parameters()), dict(ref64.named_parameters())
     for k, p in net.named_parameters():
         if p.grad is None:
             assert rp[k].grad is None, k
             continue
-        _close(p.grad, rp[k].grad, 1e-4)
-    rb = dict(ref.named_buffers())
+        check(p.grad, rp[k].grad, tp[k].grad, k)
+    rb, tb = dict(ref.named_buffers()), dict(ref64.named_buffers())
     for k, v in net.named_buffers():
         if v.dtype.is_floating_point:
-            _close(v, rb[k], 1e-5)
+            check(v, rb[k], tb[k], k)
         else:
             assert torch.equal(v, rb[k]), k
