@@ -530,7 +530,14 @@ FusedPlan fused_plan(int nseg, int max_a, int max_b, int a_total, int b_total) {
     const int qtile = 64 * p.qpt;
     p.qtiles = (max_a + qtile - 1) / qtile;
     const long long base = (long long)nseg * p.qtiles;
-    long long rs = (NF_TARGET_WAVES + base - 1) / base;
+    // The grid is sized by the host-side bounds; ragged tables usually hold far less work (the
+    // step's part family: 64 of 256 pairs non-empty, refs ~1/4 of the bound). With the buffers
+    // partitioned by the segments, a_total * b_total / nseg estimates the real pair count; plan
+    // proportionally more waves so that about NF_TARGET_WAVES of them do work (at most 4x).
+    const double est = (double)a_total * (double)b_total / (double)nseg;
+    const double ratio = est > 0.0 ? (double)pairs / est : 1.0;
+    const long long target = (long long)(NF_TARGET_WAVES * (ratio < 1.0 ? 1.0 : (ratio > 4.0 ? 4.0 : ratio)));
+    long long rs = (target + base - 1) / base;
     const long long rs_max = (max_b + 63) / 64;         // at least 64 refs per wave
     rs = rs < 1 ? 1 : (rs > rs_max ? rs_max : rs);
     int rr = (int)((max_b + rs - 1) / rs);
