@@ -90,8 +90,10 @@ class ResidualAttentionMessagePropagation(nn.Module):
         X = torch.cat([x0.reshape(R0, C), x1.reshape(B * n1, C)])
         q_, k_, v_ = mha.in_proj_q, mha.in_proj_k, mha.in_proj_v
         qkv = F.linear(X, torch.cat([mha._w(q_), mha._w(k_), mha._w(v_)]), torch.cat([q_.bias, k_.bias, v_.bias]))
-        o = torch.cat([self_attention(qkv[:R0].view(B, n0, -1), mha.num_heads).reshape(R0, C),
-                       self_attention(qkv[R0:].view(B, n1, -1), mha.num_heads).reshape(B * n1, C)])
+        R1 = B * n1
+        q0, q1 = qkv.split([R0, R1])          # split (backward: one cat) rather than slices
+        o = torch.cat([self_attention(q0.view(B, n0, -1), mha.num_heads).reshape(R0, C),
+                       self_attention(q1.view(B, n1, -1), mha.num_heads).reshape(R1, C)])
         message = F.linear(o, mha._w(mha.out_proj), mha.out_proj.bias)
         first = X - message if self.use_offset else X
         h = torch.cat([first, message], dim=-1)
@@ -101,9 +103,10 @@ class ResidualAttentionMessagePropagation(nn.Module):
             elif isinstance(layer, nn.ReLU):
                 h = F.relu(h)
             else:                                          # BatchNorm1d: one node set at a time
-                h = torch.cat([layer(h[:R0]), layer(h[R0:])])
-        out = X + h
-        return out[:R0].view(B, n0, C), out[R0:].view(B, n1, C)
+                h0, h1 = h.split([R0, R1])
+                h = torch.cat([layer(h0), layer(h1)])
+        out0, out1 = (X + h).split([R0, R1])
+        return out0.view(B, n0, C), out1.view(B, n1, C)
 
 
 class DescriptorsSelfAttention(nn.Module):

@@ -1012,9 +1012,10 @@ __device__ __forceinline__ double blk_weight(const float* gw, int grows, int b) 
 __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ ws, int M, int N,
         const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
         float* running_mean, float* running_var, float* mean_o, float* invstd_o, float* scale_o, float* shift_o,
-        const float* __restrict__ gw, int grows) {
+        const float* __restrict__ gw, int grows, long long* nbt) {
     __shared__ double sh[256], shc[256];
     const int n = blockIdx.x, t = threadIdx.x;
+    if (nbt && n == 0 && t == 0) *nbt += 1;
     const int nblk = (M + BM - 1) / BM;
     double s = 0.0, c = 0.0;
     for (int b = t; b < nblk; b += 256) {
@@ -1412,7 +1413,7 @@ int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, in
 int ured_bn_fwd_finalize(const float* stat_ws, int M, int N, const float* gamma, const float* beta,
                          float eps, float momentum, float* running_mean, float* running_var,
                          float* mean, float* invstd, float* scale, float* shift,
-                         const float* group_w, int group_rows, void* stream) {
+                         const float* group_w, int group_rows, long long* num_batches_tracked, void* stream) {
     ured::clear_error();
     URED_REQUIRE(M > 0 && N >= 0, "ured_bn_fwd_finalize: bad sizes M=%d N=%d", M, N);
     if (N == 0) return 0;
@@ -1420,7 +1421,8 @@ int ured_bn_fwd_finalize(const float* stat_ws, int M, int N, const float* gamma,
     URED_REQUIRE(!group_w || (group_rows > 0 && group_rows % BM == 0),
                  "ured_bn_fwd_finalize: row weights need group_rows multiple of %d (got %d)", BM, group_rows);
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, stat_ws, M, N, gamma, beta,
-                       eps, momentum, running_mean, running_var, mean, invstd, scale, shift, group_w, group_rows);
+                       eps, momentum, running_mean, running_var, mean, invstd, scale, shift, group_w, group_rows,
+                       num_batches_tracked);
     return ured::launch_status("ured_bn_fwd_finalize");
 }
 

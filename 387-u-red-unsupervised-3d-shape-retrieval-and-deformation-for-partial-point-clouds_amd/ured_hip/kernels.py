@@ -32,7 +32,7 @@ class GemmDesc(ctypes.Structure):
 _SIGS = {
     "ured_gemm": [ctypes.POINTER(GemmDesc), _P],
     "ured_splitk_reduce": [_P, _I, _I, _I, _P, _I, _I, _P, _P],
-    "ured_bn_fwd_finalize": [_P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "ured_bn_fwd_finalize": [_P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     "ured_bn_bwd_finalize": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P],
     "ured_bn_bwd_apply": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "ured_pool_finalize": [_P, _I, _I, _I, _P, _P, _I, _P, _P, _P],
@@ -116,7 +116,8 @@ def _rw(rw):
     return (None, 0) if rw is None else (rw.w.data_ptr(), rw.group_rows)
 
 
-def bn_fwd_finalize(stat_ws, M, N, gamma, beta, eps, momentum, running_mean, running_var, rw=None):
+def bn_fwd_finalize(stat_ws, M, N, gamma, beta, eps, momentum, running_mean, running_var, rw=None,
+                    num_batches_tracked=None):
     dev = stat_ws.device
     mean = torch.empty(N, device=dev)
     invstd = torch.empty(N, device=dev)
@@ -124,7 +125,7 @@ def bn_fwd_finalize(stat_ws, M, N, gamma, beta, eps, momentum, running_mean, run
     shift = torch.empty(N, device=dev)
     _lib.call("ured_bn_fwd_finalize", _p(stat_ws), int(M), int(N), _p(gamma), _p(beta), float(eps), float(momentum),
               _p(running_mean), _p(running_var), _p(mean), _p(invstd), _p(scale), _p(shift), *_rw(rw),
-              _lib.stream_of(stat_ws))
+              _p(num_batches_tracked), _lib.stream_of(stat_ws))
     return BNState(mean, invstd, scale, shift)
 
 

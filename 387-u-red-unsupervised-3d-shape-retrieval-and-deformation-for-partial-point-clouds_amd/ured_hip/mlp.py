@@ -40,13 +40,22 @@ class EncoderSpec:
         self.rw = rw
 
 
+def _nbt(bnm):
+    """The module's int64 num_batches_tracked (incremented inside the finalize launch)."""
+    t = bnm.num_batches_tracked
+    if t is None:
+        return None
+    if t.dtype != torch.int64 or not t.is_cuda or not t.is_contiguous():
+        raise TypeError("num_batches_tracked must be a contiguous int64 device tensor")
+    return t
+
+
 def _bn_state(spec, i, Yws, M, N, gamma, beta):
     bnm = spec.bn_modules[i]
     if spec.training:
-        if bnm.num_batches_tracked is not None:
-            bnm.num_batches_tracked.add_(1)
         mom = bnm.momentum if bnm.momentum is not None else 0.0
-        return K.bn_fwd_finalize(Yws, M, N, gamma, beta, spec.eps, mom, bnm.running_mean, bnm.running_var, rw=spec.rw)
+        return K.bn_fwd_finalize(Yws, M, N, gamma, beta, spec.eps, mom, bnm.running_mean, bnm.running_var, rw=spec.rw,
+                                 num_batches_tracked=_nbt(bnm))
     return K.bn_eval_state(gamma, beta, bnm.running_mean, bnm.running_var, spec.eps)
 
 
@@ -232,11 +241,9 @@ class ResidualNetFn(Function):
                    bias=params[4 * i + 1], epi=K.EPI_FWD, stat_ws=sws, stat_relu=True, **kw)
             bnm = bn_modules[i]
             if training:
-                if bnm.num_batches_tracked is not None:
-                    bnm.num_batches_tracked.add_(1)
                 st = K.bn_fwd_finalize(sws, M, N, params[4 * i + 2], params[4 * i + 3], BN_EPS,
                                        bnm.momentum if bnm.momentum is not None else 0.0,
-                                       bnm.running_mean, bnm.running_var, rw=rw)
+                                       bnm.running_mean, bnm.running_var, rw=rw, num_batches_tracked=_nbt(bnm))
             else:
                 st = K.bn_eval_state(params[4 * i + 2], params[4 * i + 3], bnm.running_mean, bnm.running_var, BN_EPS)
             Ys.append(Y)

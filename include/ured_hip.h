@@ -202,11 +202,13 @@ int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, in
  * Row multiplicities (unique-row training): if group_w is non-NULL, each stored row of
  * group g = row / group_rows (group_rows a multiple of 128) stands for group_w[g] identical
  * rows of the batch; statistics are those of the expanded batch (count sum_g w_g*rows_g).
- * The same (group_w, group_rows) pair goes to the two backward calls below. */
+ * The same (group_w, group_rows) pair goes to the two backward calls below.
+ * num_batches_tracked (nullable, int64 on the device) is incremented by one (the module's
+ * counter update of a training-mode forward, folded into this launch). */
 int ured_bn_fwd_finalize(const float* stat_ws, int M, int N, const float* gamma, const float* beta,
                          float eps, float momentum, float* running_mean, float* running_var,
                          float* mean, float* invstd, float* scale, float* shift,
-                         const float* group_w, int group_rows, void* stream);
+                         const float* group_w, int group_rows, long long* num_batches_tracked, void* stream);
 
 /* BN backward finalize over EPI_BNBWD partials: dbeta = sum g, dgamma = sum g*xhat
  * (fp64, fixed order; written, or added if accumulate) and the coefficients of

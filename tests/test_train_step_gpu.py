@@ -167,3 +167,18 @@ def test_fused_clip_matches_clip_grad_norm(dev):
     for name in CLIPPED:
         for p, r in zip(ts.models[name].parameters(), ref[name]):
             torch.testing.assert_close(p.grad, r, rtol=2e-6, atol=1e-9)
+
+
+def test_bn_counters_count_steps(dev):
+    """num_batches_tracked of every BatchNorm the HIP chain runs advances by one per training
+    forward (the increment is folded into the statistics-finalize launch)."""
+    ts, batch = _setup(dev)[:2]
+    bns = [(n, m) for name in ("src_encoder_all", "target_encoder_full", "re_residual_net_full")
+           for n, m in ts.models[name].named_modules() if isinstance(m, torch.nn.BatchNorm1d)]
+    before = {n: int(m.num_batches_tracked) for n, m in bns}
+    ts.step(batch)
+    ts.step(batch)
+    for n, m in bns:
+        used = int(m.num_batches_tracked) - before[n]
+        assert used in (0, 2), (n, used)      # 0: the module's unused stn1/stn2 branches
+    assert sum(int(m.num_batches_tracked) - before[n] for n, m in bns) > 0
