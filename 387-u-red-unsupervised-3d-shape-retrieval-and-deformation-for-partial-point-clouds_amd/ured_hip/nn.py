@@ -100,10 +100,11 @@ class NNSegFunction(Function):
             raise ValueError("segs must be an int32 [nseg,4] tensor")
         segs = segs.contiguous()
         dev = a.device
-        dist_a = torch.zeros(a.shape[0], device=dev, dtype=torch.float32)
-        idx_a = torch.zeros(a.shape[0], device=dev, dtype=torch.int32)
-        dist_b = torch.zeros(b.shape[0], device=dev, dtype=torch.float32)
-        idx_b = torch.zeros(b.shape[0], device=dev, dtype=torch.int32)
+        # points outside every pair read 0: one zero fill for the four outputs (views of one buffer)
+        Na, Nb = a.shape[0], b.shape[0]
+        buf = torch.zeros(2 * (Na + Nb), device=dev, dtype=torch.float32)
+        dist_a, idx_a = buf[:Na], buf[Na:2 * Na].view(torch.int32)
+        dist_b, idx_b = buf[2 * Na:2 * Na + Nb], buf[2 * Na + Nb:].view(torch.int32)
         nseg = segs.shape[0]
         if nseg:
             ws, nbytes = _workspace(nseg, int(max_a), int(max_b), a.shape[0], b.shape[0], int(dirs), dev)
@@ -119,8 +120,8 @@ class NNSegFunction(Function):
     @staticmethod
     def backward(ctx, gd_a, _gia, gd_b, _gib):
         a, b, segs, idx_a, idx_b = ctx.saved_tensors
-        ga = torch.zeros_like(a)
-        gb = torch.zeros_like(b)
+        gbuf = torch.zeros(3 * (a.shape[0] + b.shape[0]), device=a.device, dtype=a.dtype)   # one fill
+        ga, gb = gbuf[:3 * a.shape[0]].view_as(a), gbuf[3 * a.shape[0]:].view_as(b)
         if not (ctx.dirs & 1):
             gd_a = None
         if not (ctx.dirs & 2):
