@@ -34,7 +34,7 @@ from dataset import synthetic  # noqa: E402
 from dataset.dataset_utils import get_shape, get_source_info, get_source_points, get_symmetric  # noqa: E402
 from loss.basic_consistency_loss import compute_pc_consistency, compute_pc_consistency_weighted  # noqa: E402
 from loss.basic_loss import residual_retrieval_loss  # noqa: E402
-from loss.chamfer_loss import compute_cm_loss  # noqa: E402
+from loss.chamfer_loss import compute_cm_loss, compute_cm_loss_pair  # noqa: E402
 from loss.contrast_loss import compute_contrast_loss_loss  # noqa: E402
 from network.deformation_net import DeformNet_MatchingNet as DM_decoder  # noqa: E402
 from network.deformation_net import re_residual_net  # noqa: E402
@@ -150,17 +150,23 @@ class TrainStep:
         out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
         contrast_labels = torch.where(src_labels >= 0, torch.ones_like(src_labels), src_labels)
         loss = out.new_zeros(())
+        pair = cfg["use_chamfer_loss"] > 0.0 and cfg["use_symmetry_loss"] > 0.0
+        if pair:        # both chamfer families of out and of its mirror image in one launch each
+            (T["cd_loss_full"], T["cd_loss_part"]), (T["ref_cd_loss_full"], T["ref_cd_loss_part"]) = \
+                compute_cm_loss_pair(out, get_symmetric(out), x, part_x, mask_part, np_per_part=self.np_per_part)
         if cfg["use_chamfer_loss"] > 0.0:
-            T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask_part,
-                                                                   np_per_part=self.np_per_part)
+            if not pair:
+                T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask_part,
+                                                                       np_per_part=self.np_per_part)
             loss = loss + T["cd_loss_full"] * cfg["use_chamfer_loss"] + T["cd_loss_part"] * cfg["use_chamfer_part_loss"]
         if cfg["use_contrast_loss"] > 0.0:
             T["contrast_loss"] = compute_contrast_loss_loss(target_part_f, codes, contrast_labels,
                                                             cfg.get("differentiable_gather", False))
             loss = loss + T["contrast_loss"] * cfg["use_contrast_loss"]
         if cfg["use_symmetry_loss"] > 0.0:
-            T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(get_symmetric(out), x, part_x, mask_part,
-                                                                           np_per_part=self.np_per_part)
+            if not pair:
+                T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(get_symmetric(out), x, part_x,
+                                                                               mask_part, np_per_part=self.np_per_part)
             loss = loss + T["ref_cd_loss_full"] * cfg["use_symmetry_loss"]
         return loss, out, params_full
 

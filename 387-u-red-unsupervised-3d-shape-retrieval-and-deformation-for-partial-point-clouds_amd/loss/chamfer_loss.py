@@ -50,6 +50,30 @@ def _full_segments(B, S, N, k, dev, np_per_part):
     return torch.stack([ar * S, k * np_per_part, ar * N, torch.full_like(ar, N)], 1).int()
 
 
+def _doubled(parts, B, N, P):
+    """The PartBatch of cat([x, x]) (a second copy of the batch: disjoint point ranges)."""
+    off = parts.off.long()
+    return PartBatch(x_sorted=torch.cat([parts.x_sorted, parts.x_sorted]),
+                     off=torch.cat([off[:-1], off[:-1] + B * N, off[-1:] + B * N]).int(),
+                     gid=torch.cat([parts.gid, parts.gid + B * P]),
+                     counts=torch.cat([parts.counts, parts.counts]), max_parts=P)
+
+
+def compute_cm_loss_pair(source_p, source_p2, target_p, target_part, mask, np_per_part=NP_PER_PART):
+    """(compute_cm_loss(source_p, ...), compute_cm_loss(source_p2, ...)) against the same
+    target — the chamfer and symmetric-chamfer terms of the step (engine/train.py:288,302) — as
+    ONE ragged launch per family over the two stacked batches. The NN results are per segment,
+    so identical to the separate calls; the row means may round differently by an ulp."""
+    B, S, _ = source_p.shape
+    N = target_p.shape[1]
+    P = mask.shape[1]
+    parts = _as_partbatch(target_p, target_part, mask)
+    full, part = compute_cm_loss(torch.cat([source_p, source_p2]), torch.cat([target_p, target_p]),
+                                 _doubled(parts, B, N, P), torch.cat([mask, mask]), batch_reduction=None,
+                                 np_per_part=np_per_part)
+    return (full[:B].mean(), part[:B].mean()), (full[B:].mean(), part[B:].mean())
+
+
 def compute_cm_loss(source_p, target_p, target_part=None, mask=None, batch_reduction="mean",
                     np_per_part=NP_PER_PART):
     """Returns (mean_b full CD, mean_b part CD) with a mask, else chamfer_distance2 per sample.

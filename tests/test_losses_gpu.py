@@ -92,3 +92,30 @@ def test_calc_cd_dcd_fscore(dev):
     np.testing.assert_allclose(dcd.numpy(), ((l1 + l2) / 2).numpy(), rtol=1e-5)
     dd1, dd2, ii1, ii2 = chamfer_3DDist()(out.to(dev), gt.to(dev))
     assert ii1.dtype == torch.int32 and dd1.shape == (2, 400)
+
+
+def test_cm_loss_pair_equals_two_calls(dev):
+    """compute_cm_loss_pair (chamfer + symmetric chamfer in one launch per family) equals the two
+    compute_cm_loss calls: the NN results are per segment (identical); only torch's row
+    reductions over a [2B, .] instead of a [B, .] tensor and the gradient-accumulation grouping
+    may round differently (1 ulp)."""
+    from dataset.dataset_utils import get_symmetric
+    from loss.chamfer_loss import compute_cm_loss, compute_cm_loss_pair
+    from ured_hip.ops import build_parts
+    g = torch.Generator().manual_seed(3)
+    B, S, N, P = 4, 16 * 256, 512, 16
+    out0 = torch.rand(B, S, 3, generator=g).to(dev)
+    x = torch.rand(B, N, 3, generator=g).to(dev)
+    k = torch.tensor([3, 1, 16, 5])
+    labels = torch.stack([(torch.arange(N) * int(kk)) // N for kk in k]).to(dev)
+    parts = build_parts(labels, x, P)
+    a = out0.clone().requires_grad_(True)
+    b = out0.clone().requires_grad_(True)
+    (f1, p1), (f2, p2) = compute_cm_loss_pair(a, get_symmetric(a), x, parts, parts.mask, np_per_part=256)
+    r1 = compute_cm_loss(b, x, parts, parts.mask, np_per_part=256)
+    r2 = compute_cm_loss(get_symmetric(b), x, parts, parts.mask, np_per_part=256)
+    for u, v in ((f1, r1[0]), (p1, r1[1]), (f2, r2[0]), (p2, r2[1])):
+        torch.testing.assert_close(u, v, rtol=1e-6, atol=0)
+    (30 * f1 + p1 + 30 * f2).backward()
+    (30 * r1[0] + r1[1] + 30 * r2[0]).backward()
+    torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-6 * float(b.grad.abs().max()))
