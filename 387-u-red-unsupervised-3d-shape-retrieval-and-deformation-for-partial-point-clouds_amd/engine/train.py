@@ -143,7 +143,8 @@ class TrainStep:
 
     def _deform_losses(self, T, tcode, codes, mats, param_def, x, part_x, mask_part, target_part_f, src_labels):
         """param_decoder_full -> get_shape -> chamfer (full, part), contrast and symmetry terms
-        (engine/train.py:253-302) -> (their weighted sum, out, params)."""
+        (engine/train.py:253-302) -> (their weighted sum, out, params, the x -> out NN indices of
+        the chamfer full family or None)."""
         cfg, M = self.cfg, self.models
         B = x.shape[0]
         params_full = M["param_decoder_full"](tcode, codes, None)
@@ -151,9 +152,11 @@ class TrainStep:
         contrast_labels = torch.where(src_labels >= 0, torch.ones_like(src_labels), src_labels)
         loss = out.new_zeros(())
         pair = cfg["use_chamfer_loss"] > 0.0 and cfg["use_symmetry_loss"] > 0.0
+        knn_idx = None
         if pair:        # both chamfer families of out and of its mirror image in one launch each
-            (T["cd_loss_full"], T["cd_loss_part"]), (T["ref_cd_loss_full"], T["ref_cd_loss_part"]) = \
-                compute_cm_loss_pair(out, get_symmetric(out), x, part_x, mask_part, np_per_part=self.np_per_part)
+            (T["cd_loss_full"], T["cd_loss_part"]), (T["ref_cd_loss_full"], T["ref_cd_loss_part"]), knn_idx = \
+                compute_cm_loss_pair(out, get_symmetric(out), x, part_x, mask_part, np_per_part=self.np_per_part,
+                                     return_idx=True)
         if cfg["use_chamfer_loss"] > 0.0:
             if not pair:
                 T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask_part,
@@ -168,7 +171,7 @@ class TrainStep:
                 T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(get_symmetric(out), x, part_x,
                                                                                mask_part, np_per_part=self.np_per_part)
             loss = loss + T["ref_cd_loss_full"] * cfg["use_symmetry_loss"]
-        return loss, out, params_full
+        return loss, out, params_full, knn_idx
 
     def forward(self, batch, epoch=0):
         cfg, M = self.cfg, self.models
@@ -218,11 +221,11 @@ class TrainStep:
                 if torch.is_tensor(t):
                     t.record_stream(dside)
             with torch.cuda.stream(dside):
-                loss_d, out, params_full = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
-                                                               mask_part, target_part_f, src_labels)
+                loss_d, out, params_full, knn_idx = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
+                                                                        mask_part, target_part_f, src_labels)
         else:
-            loss_d, out, params_full = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
-                                                           mask_part, target_part_f, src_labels)
+            loss_d, out, params_full, knn_idx = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
+                                                                    mask_part, target_part_f, src_labels)
         recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
         re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
                                                          off=re_in.off).view(B, N, 3)
@@ -230,10 +233,14 @@ class TrainStep:
             main.wait_stream(dside)
             for t in [loss_d, out, params_full] + [v for v in T.values() if torch.is_tensor(v)]:
                 t.record_stream(main)
+            if knn_idx is not None:
+                knn_idx.record_stream(main)
         loss = loss_d
         if cfg["use_residuals_reg"] > 0.0 and epoch > cfg["init_p_m_loss"]:
+            # the x -> out NN query of the residual loss is the chamfer full family's second direction
             T["re_reg_loss_full"], T["reg_loss_full"] = residual_retrieval_loss(x, out.detach(), re_res, mask_part,
-                                                                                np_per_part=self.np_per_part)
+                                                                                np_per_part=self.np_per_part,
+                                                                                nn_idx=knn_idx)
             loss = loss + T["re_reg_loss_full"] * cfg["use_residuals_reg"] + T["reg_loss_full"] * cfg["use_residuals_reg"] * 0.01
         if cfg["use_recon"] > 0.0:
             T["recon_loss_full"] = compute_pc_consistency(recon_full_p, x)

@@ -36,11 +36,17 @@ def knn_points(p1, p2, lengths1=None, lengths2=None, K=1, return_nn=False, **_):
     return KNN(d, i, nn)
 
 
-def residual_retrieval_loss(x, x_source, residuals, mask_part=None, np_per_part=NP_PER_PART):
+def residual_retrieval_loss(x, x_source, residuals, mask_part=None, np_per_part=NP_PER_PART, nn_idx=None):
     """x [B,N,3] target, x_source [B,S,3] deformed sources (only the first k_b*1024 are valid),
-    residuals [B,N,3] -> (mean_n sum_xyz |x + r - nn|, mean_n sum_xyz |r|)."""
+    residuals [B,N,3] -> (mean_n sum_xyz |x + r - nn|, mean_n sum_xyz |r|).
+    nn_idx [B,N] (optional): the x -> x_source nearest-neighbour indices when the caller already
+    has them (the chamfer full family computes exactly this query, compute_cm_loss(return_idx))."""
     B, S, _ = x_source.shape
-    valid = (mask_part.sum(1).round().long() * np_per_part).clamp(max=S)
-    _, _, nn = knn_points(x, x_source, lengths2=valid, K=1, return_nn=True)
-    res_nn = x + residuals - nn.squeeze(2)
+    if nn_idx is None:
+        valid = (mask_part.sum(1).round().long() * np_per_part).clamp(max=S)
+        _, _, nn = knn_points(x, x_source, lengths2=valid, K=1, return_nn=True)
+        nn = nn.squeeze(2)
+    else:
+        nn = torch.gather(x_source, 1, nn_idx.long().unsqueeze(-1).expand(-1, -1, 3))
+    res_nn = x + residuals - nn
     return torch.abs(res_nn).sum(-1).mean(), torch.abs(residuals).sum(-1).mean()

@@ -59,7 +59,8 @@ def _doubled(parts, B, N, P):
                      counts=torch.cat([parts.counts, parts.counts]), max_parts=P)
 
 
-def compute_cm_loss_pair(source_p, source_p2, target_p, target_part, mask, np_per_part=NP_PER_PART):
+def compute_cm_loss_pair(source_p, source_p2, target_p, target_part, mask, np_per_part=NP_PER_PART,
+                         return_idx=False):
     """(compute_cm_loss(source_p, ...), compute_cm_loss(source_p2, ...)) against the same
     target — the chamfer and symmetric-chamfer terms of the step (engine/train.py:288,302) — as
     ONE ragged launch per family over the two stacked batches. The NN results are per segment,
@@ -68,14 +69,16 @@ def compute_cm_loss_pair(source_p, source_p2, target_p, target_part, mask, np_pe
     N = target_p.shape[1]
     P = mask.shape[1]
     parts = _as_partbatch(target_p, target_part, mask)
-    full, part = compute_cm_loss(torch.cat([source_p, source_p2]), torch.cat([target_p, target_p]),
-                                 _doubled(parts, B, N, P), torch.cat([mask, mask]), batch_reduction=None,
-                                 np_per_part=np_per_part)
-    return (full[:B].mean(), part[:B].mean()), (full[B:].mean(), part[B:].mean())
+    r = compute_cm_loss(torch.cat([source_p, source_p2]), torch.cat([target_p, target_p]),
+                        _doubled(parts, B, N, P), torch.cat([mask, mask]), batch_reduction=None,
+                        np_per_part=np_per_part, return_idx=return_idx)
+    full, part = r[0], r[1]
+    res = (full[:B].mean(), part[:B].mean()), (full[B:].mean(), part[B:].mean())
+    return res + (r[2][:B],) if return_idx else res
 
 
 def compute_cm_loss(source_p, target_p, target_part=None, mask=None, batch_reduction="mean",
-                    np_per_part=NP_PER_PART):
+                    np_per_part=NP_PER_PART, return_idx=False):
     """Returns (mean_b full CD, mean_b part CD) with a mask, else chamfer_distance2 per sample.
 
     Like the reference, target_part is used only with a mask; CD = mean(cost1) + mean(cost2).
@@ -91,7 +94,7 @@ def compute_cm_loss(source_p, target_p, target_part=None, mask=None, batch_reduc
     src = source_p.contiguous()
     # full family
     segs = _full_segments(B, S, N, k, dev, np_per_part)
-    da, _, db, _ = nn_segments(src, target_p.contiguous(), segs, S, N, 3)
+    da, _, db, ib = nn_segments(src, target_p.contiguous(), segs, S, N, 3)
     n_valid = (k * np_per_part).clamp(min=1).float()
     full = da.view(B, S).sum(1) / n_valid + db.view(B, N).mean(1)
     full = torch.where(k > 0, full, torch.full_like(full, float("nan")))
@@ -111,6 +114,9 @@ def compute_cm_loss(source_p, target_p, target_part=None, mask=None, batch_reduc
     cost2 = segment_sum(pb.view(-1, 1), parts.off, parts.gid).view(B, P) / parts.counts.clamp(min=1).float()
     part_cd = (cost1 + cost2) * valid.float()
     part = part_cd.sum(1) / k.float()
+    # return_idx: also the x -> source NN index of every target point ([B, N] int32, relative to
+    # the sample's source row) — residual_retrieval_loss's knn_points query, already computed here
+    extra = (ib.view(B, N),) if return_idx else ()
     if batch_reduction == "mean":
-        return full.mean(), part.mean()
-    return full, part
+        return (full.mean(), part.mean()) + extra
+    return (full, part) + extra

@@ -119,3 +119,23 @@ def test_cm_loss_pair_equals_two_calls(dev):
     (30 * f1 + p1 + 30 * f2).backward()
     (30 * r1[0] + r1[1] + 30 * r2[0]).backward()
     torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-6 * float(b.grad.abs().max()))
+
+
+def test_residual_loss_with_chamfer_indices(dev):
+    """residual_retrieval_loss fed the chamfer full family's x -> out indices equals its own
+    knn_points query (the same NN primitive, same direction, same valid lengths)."""
+    from loss.basic_loss import residual_retrieval_loss
+    from loss.chamfer_loss import compute_cm_loss
+    from ured_hip.ops import build_parts
+    g = torch.Generator().manual_seed(5)
+    B, S, N, P = 3, 16 * 256, 500, 16
+    out = torch.rand(B, S, 3, generator=g).to(dev)
+    x = torch.rand(B, N, 3, generator=g).to(dev)
+    r = (torch.rand(B, N, 3, generator=g) * 0.1).to(dev)
+    k = torch.tensor([2, 7, 16])
+    labels = torch.stack([(torch.arange(N) * int(kk)) // N for kk in k]).to(dev)
+    parts = build_parts(labels, x, P)
+    _, _, idx = compute_cm_loss(out, x, parts, parts.mask, np_per_part=256, return_idx=True)
+    a = residual_retrieval_loss(x, out, r, parts.mask, np_per_part=256)
+    b = residual_retrieval_loss(x, out, r, parts.mask, np_per_part=256, nn_idx=idx)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
