@@ -32,6 +32,11 @@ def get_shape(A, param, src_default_param=None, weight=1.0, param_init=None, con
         p = p + src_default_param.reshape(bs * num_part, pd, 1)
     if connectivity_mat is not None:
         p = torch.bmm(connectivity_mat, p)
+    # A [BP, 3n, 6] @ p [BP, 6, 1] is a batched GEMV (HBM-bound: 18.9 MB of A at config 2) that the
+    # BLAS libraries run as tile GEMMs (130-140 us on MI355X): one streaming HIP kernel each way
+    if pd == 6 and not A.requires_grad:             # (CPU tensors raise: no fallback)
+        from ured_hip.ops import GetShapeFn
+        return GetShapeFn.apply(A, p.reshape(bs * num_part, pd)).reshape(bs, num_part, -1, 3)
     return torch.bmm(A, p).reshape(bs, num_part, -1, 3)
 
 

@@ -28,6 +28,8 @@ _SIGNATURES = {
     "ured_nn_seg_fwd": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_nn_fwd_workspace": [_I, _I, _I, _I, _I, _I],
     "ured_seg_aabb": [_P, _P, _I, _P, _P],
+    "ured_get_shape_fwd": [_P, _P, _I, _I, _P, _P],
+    "ured_get_shape_bwd": [_P, _P, _I, _I, _P, _P],
     "ured_emd_workspace": [_I, _I],
     "ured_emd_fwd": [_P, _P, _I, _I, _F, _I, _P, _P, _P, _SZ, _P],
     "ured_emd_bwd": [_P, _P, _I, _I, _P, _P, _P, _P],

@@ -30,6 +30,51 @@ class SegmentSumFn(Function):
         return gout.index_select(0, gid.long()), None, None
 
 
+class GetShapeFn(Function):
+    """out [J, R] = A [J, R, 6] @ p [J, 6] on HIP (ured_get_shape_fwd/bwd); gradient for p only
+    (A is the source parts' data)."""
+
+    @staticmethod
+    def forward(ctx, A, p):
+        if A.requires_grad:
+            raise NotImplementedError("get_shape: gradients w.r.t. the source matrices are not supported")
+        _lib.require_device(A, p)
+        A = A.contiguous().float()
+        p = p.contiguous().float()
+        J, R, _ = A.shape
+        out = torch.empty(J, R, device=A.device, dtype=torch.float32)
+        _lib.call("ured_get_shape_fwd", _lib.ptr(A), _lib.ptr(p), J, R, _lib.ptr(out), _lib.stream_of(A))
+        ctx.save_for_backward(A)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (A,) = ctx.saved_tensors
+        J, R, _ = A.shape
+        gp = torch.empty(J, 6, device=A.device, dtype=torch.float32)
+        _lib.call("ured_get_shape_bwd", _lib.ptr(A), _lib.ptr(g.contiguous()), J, R, _lib.ptr(gp), _lib.stream_of(A))
+        return None, gp
+
+
+class PermuteRowsFn(Function):
+    """out[b, i] = x[b, perm[b, i]] for a per-sample permutation perm [B, N]; the backward is the
+    gather by the inverse permutation (torch.gather's backward would scatter_add into zeros)."""
+
+    @staticmethod
+    def forward(ctx, x, perm, inv):
+        ctx.save_for_backward(inv)
+        return torch.gather(x, 1, perm.unsqueeze(-1).expand(-1, -1, x.shape[-1]))
+
+    @staticmethod
+    def backward(ctx, g):
+        (inv,) = ctx.saved_tensors
+        return torch.gather(g, 1, inv.unsqueeze(-1).expand(-1, -1, g.shape[-1])), None, None
+
+
+def permute_rows(x, perm, inv):
+    return PermuteRowsFn.apply(x, perm, inv)
+
+
 def segment_sum(x, off, gid):
     """x [R, C], off int32 [G+1] (row ranges), gid int32 [R] (segment of each row) -> [G, C]."""
     return SegmentSumFn.apply(x, off, gid)
@@ -40,7 +85,7 @@ class PartBatch:
 
     x_sorted [B, N, 3]  points ordered by part label (stable), i.e. the
                         reference's torch.cat over part_x[b] (engine/train.py:119,133)
-    perm     [B, N]     original index of each sorted point
+    perm     [B, N]     original index of each sorted point (inv_perm: its inverse)
     gid      [B*N] i32  global part slot (b*P + rank) of each sorted point
     off      [B*P+1] i32 row offsets of each part slot in the flattened sorted rows
     counts   [B, P]     points per part slot (0 for padding slots)
@@ -69,6 +114,7 @@ def build_parts(labels, x, max_parts):
     slots = torch.arange(P, device=dev)
     mask = (slots.unsqueeze(0) < k.unsqueeze(1)).float()
     lab_sorted, perm = torch.sort(lab, dim=1, stable=True)
+    inv_perm = torch.empty_like(perm).scatter_(1, perm, torch.arange(N, device=dev).expand(B, -1))
     x_sorted = torch.gather(x, 1, perm.unsqueeze(-1).expand(-1, -1, 3))
     rank_sorted = torch.gather(rank_of_label, 1, lab_sorted)
     counts = torch.zeros(B, P, dtype=torch.int64, device=dev).scatter_add_(
@@ -77,7 +123,7 @@ def build_parts(labels, x, max_parts):
     base = (torch.arange(B, device=dev) * N).unsqueeze(1)
     off = torch.cat([(base + starts).reshape(-1), torch.full((1,), B * N, device=dev, dtype=torch.int64)]).int()
     gid = (rank_sorted + (torch.arange(B, device=dev) * P).unsqueeze(1)).reshape(-1).int()
-    return PartBatch(x_sorted=x_sorted, perm=perm, gid=gid, off=off, counts=counts, k=k, mask=mask,
+    return PartBatch(x_sorted=x_sorted, perm=perm, inv_perm=inv_perm, gid=gid, off=off, counts=counts, k=k, mask=mask,
                      rank_of_label=rank_of_label, present=present, max_parts=P)
 
 

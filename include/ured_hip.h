@@ -21,6 +21,7 @@
  *                       loss/basic_loss.py:249-265 (pytorch3d knn_points K=1),
  *                       batched into one ragged launch.
  *   ured_nn_fwd_ws / ured_nn_seg_fwd_ws <- the same two, both directions in one pass
+ *   ured_get_shape_fwd/bwd <- get_shape's torch.bmm (dataset/dataset_utils.py:691-726)
  *   ured_emd_fwd / ured_emd_bwd <- emd.forward / emd.backward (utils_v2/metrics/EMD/emd.cpp:14-24)
  *   ured_nn_seg_bwd  <- autograd of the above (NmDistanceGradKernel semantics,
  *                       chamfer3D.cu:155-174, made deterministic).
@@ -87,6 +88,12 @@ int ured_nn_seg_fwd_ws(const float* a, const float* b, const int* segs, int nseg
                        int max_a_len, int max_b_len, int dirs, int a_total, int b_total,
                        float* dist_a, int* idx_a, float* dist_b, int* idx_b,
                        void* workspace, size_t ws_bytes, void* stream);
+
+/* get_shape (dataset/dataset_utils.py:691-726): out[j, r] = sum_k A[j, r, k] p[j, k] for every
+ * part slot j (A [nparts, rows, 6] contiguous, 8-byte aligned; p [nparts, 6] = weight*param +
+ * default); the backward gives grad_p[j, k] = sum_r A[j, r, k] grad_out[j, r] (deterministic). */
+int ured_get_shape_fwd(const float* A, const float* p, int nparts, int rows, float* out, void* stream);
+int ured_get_shape_bwd(const float* A, const float* grad_out, int nparts, int rows, float* grad_p, void* stream);
 
 /* Per-part axis-aligned boxes (compute_aabbox, dataset/dataset_utils.py:77-85, as used by
  * get_part, engine/train.py:119-128): x [R,3] points sorted by segment, off int32 [G+1] row

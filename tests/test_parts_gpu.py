@@ -36,3 +36,26 @@ def test_part_aabb_rejects_cpu():
     pb = PartBatch(x_sorted=torch.zeros(1, 4, 3), off=torch.zeros(2, dtype=torch.int32), max_parts=1)
     with pytest.raises(RuntimeError):
         part_aabb(pb)
+
+
+def test_get_shape_hip_matches_bmm(dev):
+    """get_shape's HIP GEMV (ured_get_shape_fwd/bwd) vs the float64 torch.bmm of the reference
+    formula (dataset_utils.py:691-726), values and the gradient w.r.t. the params; deterministic."""
+    from dataset.dataset_utils import get_shape
+    g = torch.Generator().manual_seed(0)
+    B, P, R = 4, 16, 3 * 1024
+    A = torch.randn(B, P, R, 6, generator=g).to(dev)
+    prm = torch.randn(B, P, 6, generator=g).to(dev).requires_grad_(True)
+    dflt = torch.randn(B, P, 6, generator=g).to(dev)
+    out = get_shape(A, prm, dflt, 0.1)
+    p64 = (0.1 * prm.detach().double() + dflt.double()).view(B * P, 6, 1)
+    ref = torch.bmm(A.double().view(B * P, R, 6), p64).view(B, P, -1, 3)
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-5)
+    go = torch.randn(out.shape, generator=g).to(dev)
+    out.backward(go)
+    gref = 0.1 * torch.bmm(A.double().view(B * P, R, 6).transpose(1, 2), go.double().view(B * P, R, 1)).view(B, P, 6)
+    torch.testing.assert_close(prm.grad.double(), gref, rtol=1e-4, atol=1e-4)
+    g1 = prm.grad.clone()
+    prm.grad = None
+    get_shape(A, prm, dflt, 0.1).backward(go)
+    assert torch.equal(prm.grad, g1)
