@@ -1000,6 +1000,52 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     }
 }
 
+// ---- skinny weight gradient: ws[blk][co][ki] = sum over the block's rows of dY[m][co] * pro(X[m][ki]),
+// for the edge layers where min(Cout, Kin) <= 4 (3-channel inputs / outputs): a 128x128 MFMA tile
+// would be almost all padding. Thread (j, lane): j indexes the wide side, lanes stride the rows;
+// the lanes of a column combine in LDS in a fixed order, the blocks in ured_splitk_reduce's.
+constexpr int SK_ROWS = 256;
+
+template <int PRO, bool SMALL_IS_OUT>
+__global__ __launch_bounds__(256) void wgrad_skinny_kernel(const float* __restrict__ dY, int ldd,
+        const float* __restrict__ X, int ldx, int Cout, int Kin, int M, const float* __restrict__ ps,
+        const float* __restrict__ pt, float* __restrict__ ws) {
+    __shared__ float red[256][4];
+    const int D = SMALL_IS_OUT ? Kin : Cout, S = SMALL_IS_OUT ? Cout : Kin;
+    const int t = threadIdx.x, j = t % D, lane = t / D, lanes = 256 / D;
+    const bool active = lane < lanes;
+    const int r0 = blockIdx.x * SK_ROWS, r1 = min(M, r0 + SK_ROWS);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (active) {
+        const float sj = (PRO != URED_PRO_NONE && SMALL_IS_OUT) ? ps[j] : 0.f;
+        const float tj = (PRO != URED_PRO_NONE && SMALL_IS_OUT) ? pt[j] : 0.f;
+        for (int m = r0 + lane; m < r1; m += lanes) {
+            const float big = SMALL_IS_OUT ? pro_v<PRO>(X[(size_t)m * ldx + j], sj, tj) : dY[(size_t)m * ldd + j];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (q >= S) break;
+                const float small = SMALL_IS_OUT ? dY[(size_t)m * ldd + q]
+                                                 : pro_v<PRO>(X[(size_t)m * ldx + q],
+                                                              PRO != URED_PRO_NONE ? ps[q] : 0.f,
+                                                              PRO != URED_PRO_NONE ? pt[q] : 0.f);
+                acc[q] = __builtin_fmaf(small, big, acc[q]);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[t][q] = acc[q];
+    __syncthreads();
+    if (!active || lane != 0) return;
+    for (int l = 1; l < lanes; ++l)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += red[l * D + j][q];
+    float* w = ws + (size_t)blockIdx.x * Cout * Kin;
+    for (int q = 0; q < S; ++q) {
+        if (SMALL_IS_OUT) w[(size_t)q * Kin + j] = acc[q];
+        else w[(size_t)j * Kin + q] = acc[q];
+    }
+}
+
 // one block (256 threads) per column; fp64 fixed-order tree reductions
 // Row multiplicities (unique-row training, see DESIGN "unique source encoding"): when gw is
 // non-null, every row of group g = row / grows stands for gw[g] identical rows of the full
@@ -1395,6 +1441,29 @@ int ured_gemm(const UredGemmDesc* dp, void* stream) {
     int rc = dispatch(d, (hipStream_t)stream);
     if (rc) return rc;
     return ured::launch_status("ured_gemm");
+}
+
+int ured_wgrad_skinny(const float* dY, int ldd, const float* X, int ldx, int Cout, int Kin, int M, int pro,
+                      const float* pro_s, const float* pro_t, float* ws, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(M >= 0 && Cout > 0 && Kin > 0, "ured_wgrad_skinny: bad sizes");
+    const bool small_out = Cout <= 4;
+    const int D = small_out ? Kin : Cout;
+    URED_REQUIRE((small_out || Kin <= 4) && D <= 256, "ured_wgrad_skinny: needs min(Cout,Kin) <= 4 and max <= 256 (got %d x %d)", Cout, Kin);
+    URED_REQUIRE(pro >= URED_PRO_NONE && pro <= URED_PRO_RES, "ured_wgrad_skinny: bad prologue %d", pro);
+    URED_REQUIRE(pro == URED_PRO_NONE || (pro_s && pro_t), "ured_wgrad_skinny: prologue needs scale/shift");
+    if (M == 0) return 0;
+    URED_REQUIRE(dY && X && ws, "ured_wgrad_skinny: null pointer");
+    const dim3 grid((M + SK_ROWS - 1) / SK_ROWS);
+    hipStream_t st = (hipStream_t)stream;
+#define URED_SK(P, SO) hipLaunchKernelGGL((wgrad_skinny_kernel<P, SO>), grid, dim3(256), 0, st, dY, ldd, X, ldx, Cout, Kin, M, pro_s, pro_t, ws)
+    if (small_out) {
+        if (pro == URED_PRO_ENC) URED_SK(URED_PRO_ENC, true); else if (pro == URED_PRO_RES) URED_SK(URED_PRO_RES, true); else URED_SK(URED_PRO_NONE, true);
+    } else {
+        if (pro == URED_PRO_ENC) URED_SK(URED_PRO_ENC, false); else if (pro == URED_PRO_RES) URED_SK(URED_PRO_RES, false); else URED_SK(URED_PRO_NONE, false);
+    }
+#undef URED_SK
+    return ured::launch_status("ured_wgrad_skinny");
 }
 
 int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, int ldo, int accumulate,

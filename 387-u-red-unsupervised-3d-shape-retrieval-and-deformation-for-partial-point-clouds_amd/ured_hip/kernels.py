@@ -32,6 +32,7 @@ class GemmDesc(ctypes.Structure):
 _SIGS = {
     "ured_gemm": [ctypes.POINTER(GemmDesc), _P],
     "ured_splitk_reduce": [_P, _I, _I, _I, _P, _I, _I, _P, _P],
+    "ured_wgrad_skinny": [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P],
     "ured_bn_fwd_finalize": [_P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     "ured_bn_bwd_finalize": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P],
     "ured_bn_bwd_apply": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
@@ -221,6 +222,13 @@ def choose_splits(Mo, No, K):
 def wgrad(dY, ldd, X, ldx, Cout, Kin, Mrows, out, ldo, *, out_off=0, X_off=0, pro=PRO_NONE, pro_s=None,
           pro_t=None, accumulate=False):
     """out[cout][kin] (+)= sum_m dY[m][cout] * pro(X[m][kin]) (split-K over the Mrows points)."""
+    if min(Cout, Kin) <= 4 and max(Cout, Kin) <= 256:     # 3-channel edge layers: no MFMA tile
+        nb = (Mrows + 255) // 256
+        ws = torch.empty(nb, Cout, Kin, device=dY.device)
+        _lib.call("ured_wgrad_skinny", _p(dY), int(ldd), _addr(X, X_off), int(ldx), int(Cout), int(Kin), int(Mrows),
+                  int(pro), _p(pro_s), _p(pro_t), _p(ws), _lib.stream_of(dY))
+        splitk_reduce(ws, nb, Cout, Kin, out, ldo, accumulate, out_off)
+        return
     splits = choose_splits(Cout, Kin, Mrows)
     if splits == 1 and not accumulate:
         gemm(Cout, Kin, Mrows, dY, ldd, X, ldx, out, ldo, a_kmajor=True, b_kmajor=True, pro_b=pro,

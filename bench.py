@@ -79,8 +79,10 @@ class DominantTimer:
     def summary(self):
         torch.cuda.synchronize()
         ms = [e0.elapsed_time(e1) for _, _, e0, e1 in self.rec]
+        # per-launch attainable time: max(FLOP / MFMA peak, algorithmic bytes / HBM peak)
+        att = sum(max(f / (PEAK_FP32_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9)) for f, b, _, _ in self.rec) * 1e3
         return {"launches": len(ms), "ms": sum(ms), "flop": sum(r[0] for r in self.rec),
-                "bytes": sum(r[1] for r in self.rec)}
+                "bytes": sum(r[1] for r in self.rec), "attainable_ms": att}
 
 
 class GemmTimer:
@@ -433,6 +435,12 @@ def main():
                     "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
                     "kernel": dom_key, "launches_per_step": round(lps, 2), "avg_launch_ms": round(avg_ms, 4),
                     "flop_per_launch": round(flop_per_launch), "timing": timing}
+        if "attainable_ms" in d:
+            # the same launches against the per-launch roofline min(MFMA peak, AI x HBM peak): the
+            # small-K shapes of this kernel sit near the ridge (AI ~ 20-40 FLOP/B)
+            att_tf = d["flop"] / (d["attainable_ms"] * 1e-3) / 1e12
+            roofline["attainable_tflops"] = round(att_tf, 2)
+            roofline["frac_of_attainable"] = round(ach / att_tf, 4)
     if breakdown:
         tot_ms = sum(v["ms"] for v in breakdown.values())
         tot_flop = sum(v["flop"] for v in breakdown.values())

@@ -218,3 +218,26 @@ def test_residual_net_plain_forward(dev):
     g = torch.Generator().manual_seed(12)
     f = torch.randn(2, 80, 128, generator=g)
     close(rn(f.to(dev)), ured_ref.residual_net(P["recon_decoder_full"], f), 2e-4, "plain")
+
+
+@pytest.mark.parametrize("Cout,Kin,pro,M", [(3, 32, 0, 70001), (64, 3, 0, 4099), (3, 64, 1, 20000),
+                                            (3, 128, 2, 513), (256, 4, 0, 255), (5, 3, 1, 1000)])
+def test_wgrad_skinny_edge_layers(K, dev, Cout, Kin, pro, M):
+    """The 3-channel edge layers' weight gradients (ured_wgrad_skinny): strided dY/X views,
+    a column offset into X, the encoder prologues, accumulate into an existing gradient."""
+    g = torch.Generator().manual_seed(Cout * 1000 + Kin + pro)
+    ldd, ldx, xoff = Cout + 5, Kin + 7, 3
+    dY = torch.randn(M, ldd, generator=g)
+    X = torch.randn(M, ldx, generator=g)
+    s, t = torch.rand(Kin, generator=g) + 0.5, torch.randn(Kin, generator=g)
+    prev = torch.randn(Cout, Kin, generator=g)
+    x = X[:, xoff:xoff + Kin].double()
+    h = {0: x, 1: torch.relu(x * s.double() + t.double()), 2: torch.relu(x) * s.double() + t.double()}[pro]
+    ref = dY[:, :Cout].double().t() @ h
+    out = torch.empty(Cout, Kin, device=dev)
+    kw = dict(pro=pro, pro_s=s.to(dev), pro_t=t.to(dev)) if pro else {}
+    K.wgrad(dY.to(dev), ldd, X.to(dev), ldx, Cout, Kin, M, out, Kin, X_off=xoff, **kw)
+    close(out, ref, 1e-5, "wgrad skinny")
+    acc = prev.to(dev)
+    K.wgrad(dY.to(dev), ldd, X.to(dev), ldx, Cout, Kin, M, acc, Kin, X_off=xoff, accumulate=True, **kw)
+    close(acc, ref + prev.double(), 1e-5, "wgrad skinny accumulate")

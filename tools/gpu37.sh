@@ -1,0 +1,13 @@
+# skinny wgrad: whole GPU suite + bench (roofline with attainable fields)
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_all.log 2>&1 || { tail -30 gpurun_out/t_all.log; exit 1; }
+tail -1 gpurun_out/t_all.log
+rm -f gpurun_out/cmp.txt
+for m in "" "--graph" ""; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-all-slots-rate --no-breakdown --no-extras --steps 30 $m > gpurun_out/b.log 2>&1 || { echo "FAIL $m"; tail -20 gpurun_out/b.log; exit 1; }
+  echo "$m $(tail -1 gpurun_out/b.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["loss"], json.dumps(d["roofline"]))')" >> gpurun_out/cmp.txt
+done
+cat gpurun_out/cmp.txt
