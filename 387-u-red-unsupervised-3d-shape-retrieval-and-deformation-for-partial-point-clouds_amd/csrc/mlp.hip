@@ -1000,49 +1000,113 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     }
 }
 
-// ---- skinny weight gradient: ws[blk][co][ki] = sum over the block's rows of dY[m][co] * pro(X[m][ki]),
-// for the edge layers where min(Cout, Kin) <= 4 (3-channel inputs / outputs): a 128x128 MFMA tile
-// would be almost all padding. Thread (j, lane): j indexes the wide side, lanes stride the rows;
-// the lanes of a column combine in LDS in a fixed order, the blocks in ured_splitk_reduce's.
-constexpr int SK_ROWS = 256;
+// ---- skinny weight gradient: out[co][ki] (+)= sum_m dY[m][co] * pro(X[m][ki]) for the edge layers
+// where min(Cout, Kin) <= 4 (3-channel inputs / outputs): a 128x128 MFMA tile would be almost all
+// padding, so this is a streaming reduction. The wide side D is spread over tpr = D/VEC threads
+// (float4 loads when aligned), 256/tpr rows go at once, SK_UNROLL rows per thread in flight; each
+// of <= SK_MAX_BLOCKS row blocks combines its lanes in LDS in a fixed order and writes one partial,
+// then skinny_reduce_kernel sums the partials of each output in a fixed tree (deterministic).
+constexpr int SK_MAX_BLOCKS = 256, SK_UNROLL = 4;
 
-template <int PRO, bool SMALL_IS_OUT>
+template <int PRO, bool SMALL_IS_OUT, int S, int VEC>
 __global__ __launch_bounds__(256) void wgrad_skinny_kernel(const float* __restrict__ dY, int ldd,
-        const float* __restrict__ X, int ldx, int Cout, int Kin, int M, const float* __restrict__ ps,
+        const float* __restrict__ X, int ldx, int D, int M, int rows_per_block, const float* __restrict__ ps,
         const float* __restrict__ pt, float* __restrict__ ws) {
-    __shared__ float red[256][4];
-    const int D = SMALL_IS_OUT ? Kin : Cout, S = SMALL_IS_OUT ? Cout : Kin;
-    const int t = threadIdx.x, j = t % D, lane = t / D, lanes = 256 / D;
-    const bool active = lane < lanes;
-    const int r0 = blockIdx.x * SK_ROWS, r1 = min(M, r0 + SK_ROWS);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (active) {
-        const float sj = (PRO != URED_PRO_NONE && SMALL_IS_OUT) ? ps[j] : 0.f;
-        const float tj = (PRO != URED_PRO_NONE && SMALL_IS_OUT) ? pt[j] : 0.f;
-        for (int m = r0 + lane; m < r1; m += lanes) {
-            const float big = SMALL_IS_OUT ? pro_v<PRO>(X[(size_t)m * ldx + j], sj, tj) : dY[(size_t)m * ldd + j];
+    __shared__ float red[256 * VEC * S];
+    const int tpr = D / VEC;
+    const int t = threadIdx.x, jv = t % tpr, lane = t / tpr, lanes = 256 / tpr;
+    const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+    float acc[VEC][S];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (q >= S) break;
-                const float small = SMALL_IS_OUT ? dY[(size_t)m * ldd + q]
-                                                 : pro_v<PRO>(X[(size_t)m * ldx + q],
-                                                              PRO != URED_PRO_NONE ? ps[q] : 0.f,
-                                                              PRO != URED_PRO_NONE ? pt[q] : 0.f);
-                acc[q] = __builtin_fmaf(small, big, acc[q]);
+    for (int v = 0; v < VEC; ++v)
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[v][q] = 0.f;
+    float bs[VEC], bt[VEC], ss[S], st[S];     // prologue scale/shift of the X side
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+        bs[v] = (PRO != URED_PRO_NONE && SMALL_IS_OUT) ? ps[jv * VEC + v] : 0.f;
+        bt[v] = (PRO != URED_PRO_NONE && SMALL_IS_OUT) ? pt[jv * VEC + v] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+        ss[q] = (PRO != URED_PRO_NONE && !SMALL_IS_OUT) ? ps[q] : 0.f;
+        st[q] = (PRO != URED_PRO_NONE && !SMALL_IS_OUT) ? pt[q] : 0.f;
+    }
+    auto load = [&](int m, float (&big)[VEC], float (&small)[S]) {
+        const float* bp = SMALL_IS_OUT ? X + (size_t)m * ldx + jv * VEC : dY + (size_t)m * ldd + jv * VEC;
+        if constexpr (VEC == 4) {
+            const float4 f = *reinterpret_cast<const float4*>(bp);
+            big[0] = f.x; big[1] = f.y; big[2] = f.z; big[3] = f.w;
+        } else {
+            big[0] = bp[0];
+        }
+        const float* sp = SMALL_IS_OUT ? dY + (size_t)m * ldd : X + (size_t)m * ldx;
+#pragma unroll
+        for (int q = 0; q < S; ++q) small[q] = sp[q];
+    };
+    auto accum = [&](float (&big)[VEC], float (&small)[S]) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+            const float bv = SMALL_IS_OUT ? pro_v<PRO>(big[v], bs[v], bt[v]) : big[v];
+#pragma unroll
+            for (int q = 0; q < S; ++q) {
+                const float sv = SMALL_IS_OUT ? small[q] : pro_v<PRO>(small[q], ss[q], st[q]);
+                acc[v][q] = __builtin_fmaf(sv, bv, acc[v][q]);
             }
+        }
+    };
+    if (lane < lanes) {
+        int m = r0 + lane;
+        for (; m + (SK_UNROLL - 1) * lanes < r1; m += SK_UNROLL * lanes) {
+            float big[SK_UNROLL][VEC], small[SK_UNROLL][S];
+#pragma unroll
+            for (int u = 0; u < SK_UNROLL; ++u) load(m + u * lanes, big[u], small[u]);
+#pragma unroll
+            for (int u = 0; u < SK_UNROLL; ++u) accum(big[u], small[u]);
+        }
+        for (; m < r1; m += lanes) {
+            float big[VEC], small[S];
+            load(m, big, small);
+            accum(big, small);
         }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) red[t][q] = acc[q];
+    for (int v = 0; v < VEC; ++v)
+#pragma unroll
+        for (int q = 0; q < S; ++q) red[(t * VEC + v) * S + q] = acc[v][q];
     __syncthreads();
-    if (!active || lane != 0) return;
+    if (lane != 0) return;
     for (int l = 1; l < lanes; ++l)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] += red[l * D + j][q];
-    float* w = ws + (size_t)blockIdx.x * Cout * Kin;
-    for (int q = 0; q < S; ++q) {
-        if (SMALL_IS_OUT) w[(size_t)q * Kin + j] = acc[q];
-        else w[(size_t)j * Kin + q] = acc[q];
+        for (int v = 0; v < VEC; ++v)
+#pragma unroll
+            for (int q = 0; q < S; ++q) acc[v][q] += red[((l * tpr + jv) * VEC + v) * S + q];
+    float* w = ws + (size_t)blockIdx.x * D * S;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            const int j = jv * VEC + v;
+            w[SMALL_IS_OUT ? q * D + j : j * S + q] = acc[v][q];       // [Cout][Kin] per block
+        }
+}
+
+// one block per output element: the row-block partials in a fixed tree order
+__global__ __launch_bounds__(256) void skinny_reduce_kernel(const float* __restrict__ ws, int nb, int total, int N,
+                                                            float* __restrict__ out, int ldo, int accumulate) {
+    __shared__ float red[256];
+    const int e = blockIdx.x, t = threadIdx.x;
+    float a = 0.f;
+    for (int z = t; z < nb; z += 256) a += ws[(size_t)z * total + e];
+    red[t] = a;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h) red[t] += red[t + h];
+        __syncthreads();
+    }
+    if (t == 0) {
+        float* o = out + (size_t)(e / N) * ldo + e % N;
+        *o = accumulate ? *o + red[0] : red[0];
     }
 }
 
@@ -1162,16 +1226,18 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     if (colsum) colsum[(size_t)blk * N + n] = s;
 }
 
-// float4 form (N, ld multiples of 4, 16-B aligned bases): block = 64 column quads x 4 row
-// lanes; lane row ty walks rows r0+ty, r0+ty+4, ... so every row read is 1 KB contiguous per
-// wave, 8 rows in flight per lane; the 4 row lanes' column sums combine in LDS in fixed order.
-__global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restrict__ G, const float* __restrict__ Y,
-        int M, int N, int ld, int res, const float* __restrict__ mean, const float* __restrict__ ca,
-        const float* __restrict__ cb, const float* __restrict__ cc, float* __restrict__ dY, float* __restrict__ colsum,
-        const float* __restrict__ gw, int grows) {
-    __shared__ float4 part[4][64];
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int n = (blockIdx.x * 64 + tx) * 4;
+// float4 form (N, ld multiples of 4, 16-B aligned bases): a block covers one 128-row partial
+// block x 64 columns with 512 threads = 16 column quads x 32 row lanes, so each lane has its 4
+// rows' loads in flight at once and narrow layers (N = 64) keep every lane busy; wave loads are
+// 4 rows x 256 B contiguous. The 32 row lanes' column sums combine in LDS in a fixed order.
+constexpr int BBA_CQ = 16, BBA_RL = 32;
+__global__ __launch_bounds__(BBA_CQ * BBA_RL) void bn_bwd_apply4_kernel(const float* __restrict__ G,
+        const float* __restrict__ Y, int M, int N, int ld, int res, const float* __restrict__ mean,
+        const float* __restrict__ ca, const float* __restrict__ cb, const float* __restrict__ cc,
+        float* __restrict__ dY, float* __restrict__ colsum, const float* __restrict__ gw, int grows) {
+    __shared__ float4 part[BBA_RL][BBA_CQ];
+    const int tx = threadIdx.x % BBA_CQ, ty = threadIdx.x / BBA_CQ;
+    const int n = (blockIdx.x * BBA_CQ + tx) * 4;
     const int blk = blockIdx.y;
     const bool nv = n < N;
     const int nn = nv ? n : 0;
@@ -1189,18 +1255,29 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
         return (res && !(y > 0.f)) ? 0.f : v;
     };
     if (nv) {
-#pragma unroll 8
-        for (int r = r0 + ty; r < r1; r += 4) {
-            const size_t e = (size_t)r * ld + n;
-            const float4 y = *reinterpret_cast<const float4*>(Y + e);
-            const float4 g = *reinterpret_cast<const float4*>(G + e);
-            float4 v;
-            v.x = one(y.x, g.x, a.x, b.x, c.x, mu.x);
-            v.y = one(y.y, g.y, a.y, b.y, c.y, mu.y);
-            v.z = one(y.z, g.z, a.z, b.z, c.z, mu.z);
-            v.w = one(y.w, g.w, a.w, b.w, c.w, mu.w);
-            *reinterpret_cast<float4*>(dY + e) = v;
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        constexpr int RPL = BM / BBA_RL;
+        float4 y[RPL], g[RPL];
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) {
+            const int r = r0 + ty + i * BBA_RL;
+            if (r < r1) {
+                const size_t e = (size_t)r * ld + n;
+                y[i] = *reinterpret_cast<const float4*>(Y + e);
+                g[i] = *reinterpret_cast<const float4*>(G + e);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) {
+            const int r = r0 + ty + i * BBA_RL;
+            if (r < r1) {
+                float4 v;
+                v.x = one(y[i].x, g[i].x, a.x, b.x, c.x, mu.x);
+                v.y = one(y[i].y, g[i].y, a.y, b.y, c.y, mu.y);
+                v.z = one(y[i].z, g[i].z, a.z, b.z, c.z, mu.z);
+                v.w = one(y[i].w, g[i].w, a.w, b.w, c.w, mu.w);
+                *reinterpret_cast<float4*>(dY + (size_t)r * ld + n) = v;
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
         }
     }
     if (!colsum) return;
@@ -1208,8 +1285,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(const float* __restr
     __syncthreads();
     if (ty == 0 && nv) {
         float4 t = part[0][tx];
-#pragma unroll
-        for (int q = 1; q < 4; ++q) {
+        for (int q = 1; q < BBA_RL; ++q) {
             const float4 u = part[q][tx];
             t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
         }
@@ -1444,25 +1520,44 @@ int ured_gemm(const UredGemmDesc* dp, void* stream) {
 }
 
 int ured_wgrad_skinny(const float* dY, int ldd, const float* X, int ldx, int Cout, int Kin, int M, int pro,
-                      const float* pro_s, const float* pro_t, float* ws, void* stream) {
+                      const float* pro_s, const float* pro_t, float* out, int ldo, int accumulate, float* ws,
+                      void* stream) {
     ured::clear_error();
-    URED_REQUIRE(M >= 0 && Cout > 0 && Kin > 0, "ured_wgrad_skinny: bad sizes");
-    const bool small_out = Cout <= 4;
-    const int D = small_out ? Kin : Cout;
-    URED_REQUIRE((small_out || Kin <= 4) && D <= 256, "ured_wgrad_skinny: needs min(Cout,Kin) <= 4 and max <= 256 (got %d x %d)", Cout, Kin);
+    URED_REQUIRE(M >= 0 && Cout > 0 && Kin > 0 && ldo >= Kin, "ured_wgrad_skinny: bad sizes");
+    const bool so = Cout <= 4;
+    const int D = so ? Kin : Cout, S = so ? Cout : Kin;
+    URED_REQUIRE((so || Kin <= 4) && D <= 256,
+                 "ured_wgrad_skinny: needs min(Cout,Kin) <= 4 and max <= 256 (got %d x %d)", Cout, Kin);
     URED_REQUIRE(pro >= URED_PRO_NONE && pro <= URED_PRO_RES, "ured_wgrad_skinny: bad prologue %d", pro);
     URED_REQUIRE(pro == URED_PRO_NONE || (pro_s && pro_t), "ured_wgrad_skinny: prologue needs scale/shift");
-    if (M == 0) return 0;
-    URED_REQUIRE(dY && X && ws, "ured_wgrad_skinny: null pointer");
-    const dim3 grid((M + SK_ROWS - 1) / SK_ROWS);
+    URED_REQUIRE(out && ws, "ured_wgrad_skinny: null pointer");
     hipStream_t st = (hipStream_t)stream;
-#define URED_SK(P, SO) hipLaunchKernelGGL((wgrad_skinny_kernel<P, SO>), grid, dim3(256), 0, st, dY, ldd, X, ldx, Cout, Kin, M, pro_s, pro_t, ws)
-    if (small_out) {
-        if (pro == URED_PRO_ENC) URED_SK(URED_PRO_ENC, true); else if (pro == URED_PRO_RES) URED_SK(URED_PRO_RES, true); else URED_SK(URED_PRO_NONE, true);
-    } else {
-        if (pro == URED_PRO_ENC) URED_SK(URED_PRO_ENC, false); else if (pro == URED_PRO_RES) URED_SK(URED_PRO_RES, false); else URED_SK(URED_PRO_NONE, false);
+    if (M == 0) {
+        if (!accumulate)
+            for (int r = 0; r < Cout; ++r)
+                if (hipMemsetAsync(out + (size_t)r * ldo, 0, sizeof(float) * Kin, st) != hipSuccess)
+                    return ured::launch_status("ured_wgrad_skinny");
+        return ured::launch_status("ured_wgrad_skinny");
     }
+    URED_REQUIRE(dY && X, "ured_wgrad_skinny: null pointer");
+    const float* big = so ? X : dY;
+    const int ldb = so ? ldx : ldd;
+    const bool vec = D % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)big & 15) == 0;
+    const int nb = std::min(SK_MAX_BLOCKS, (M + 63) / 64), rpb = (M + nb - 1) / nb;
+#define URED_SK(P, SO, SS, V) hipLaunchKernelGGL((wgrad_skinny_kernel<P, SO, SS, V>), dim3(nb), dim3(256), 0, st, \
+                                                   dY, ldd, X, ldx, D, M, rpb, pro_s, pro_t, ws)
+#define URED_SK_V(P, SO, SS) do { if (vec) URED_SK(P, SO, SS, 4); else URED_SK(P, SO, SS, 1); } while (0)
+#define URED_SK_S(P, SO) do { switch (S) { case 1: URED_SK_V(P, SO, 1); break; case 2: URED_SK_V(P, SO, 2); break; \
+                                           case 3: URED_SK_V(P, SO, 3); break; default: URED_SK_V(P, SO, 4); } } while (0)
+#define URED_SK_P(SO) do { if (pro == URED_PRO_ENC) URED_SK_S(URED_PRO_ENC, SO); \
+                           else if (pro == URED_PRO_RES) URED_SK_S(URED_PRO_RES, SO); else URED_SK_S(URED_PRO_NONE, SO); } while (0)
+    if (so) URED_SK_P(true); else URED_SK_P(false);
+#undef URED_SK_P
+#undef URED_SK_S
+#undef URED_SK_V
 #undef URED_SK
+    hipLaunchKernelGGL(skinny_reduce_kernel, dim3(Cout * Kin), dim3(256), 0, st, ws, nb, Cout * Kin, Kin, out, ldo,
+                       accumulate);
     return ured::launch_status("ured_wgrad_skinny");
 }
 
@@ -1522,8 +1617,8 @@ int ured_bn_bwd_apply(const float* G, const float* Y, int M, int N, int ld, int 
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (N % 4 == 0 && ld % 4 == 0 && al16(G) && al16(Y) && al16(dY) && al16(mean) && al16(coef_a) &&
         al16(coef_b) && al16(coef_c) && (!colsum_ws || al16(colsum_ws))) {
-        dim3 grid((N / 4 + 63) / 64, (M + BM - 1) / BM);
-        hipLaunchKernelGGL(bn_bwd_apply4_kernel, grid, dim3(256), 0, (hipStream_t)stream, G, Y, M, N, ld, res, mean,
+        dim3 grid((N / 4 + BBA_CQ - 1) / BBA_CQ, (M + BM - 1) / BM);
+        hipLaunchKernelGGL(bn_bwd_apply4_kernel, grid, dim3(BBA_CQ * BBA_RL), 0, (hipStream_t)stream, G, Y, M, N, ld, res, mean,
                            coef_a, coef_b, coef_c, dY, colsum_ws, group_w, group_rows);
     } else {
         dim3 grid((N + 255) / 256, (M + BM - 1) / BM);

@@ -32,7 +32,7 @@ class GemmDesc(ctypes.Structure):
 _SIGS = {
     "ured_gemm": [ctypes.POINTER(GemmDesc), _P],
     "ured_splitk_reduce": [_P, _I, _I, _I, _P, _I, _I, _P, _P],
-    "ured_wgrad_skinny": [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P],
+    "ured_wgrad_skinny": [_P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _P, _P],
     "ured_bn_fwd_finalize": [_P, _I, _I, _P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     "ured_bn_bwd_finalize": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P],
     "ured_bn_bwd_apply": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
@@ -204,6 +204,9 @@ def colsum(X):
     return group_colsum(X, N, 1, group_rows=R)[0]
 
 
+SKINNY_WS_BLOCKS = 256          # URED_SKINNY_WS_BLOCKS (include/ured_hip.h)
+
+
 def splitk_reduce(ws, splits, M, N, out, ldo, accumulate=False, out_off=0, bias=None):
     _lib.call("ured_splitk_reduce", _p(ws), int(splits), int(M), int(N), _addr(out, out_off), int(ldo),
               int(bool(accumulate)), _p(bias), _lib.stream_of(out))
@@ -223,11 +226,10 @@ def wgrad(dY, ldd, X, ldx, Cout, Kin, Mrows, out, ldo, *, out_off=0, X_off=0, pr
           pro_t=None, accumulate=False):
     """out[cout][kin] (+)= sum_m dY[m][cout] * pro(X[m][kin]) (split-K over the Mrows points)."""
     if min(Cout, Kin) <= 4 and max(Cout, Kin) <= 256:     # 3-channel edge layers: no MFMA tile
-        nb = (Mrows + 255) // 256
-        ws = torch.empty(nb, Cout, Kin, device=dY.device)
+        ws = torch.empty(SKINNY_WS_BLOCKS * Cout * Kin, device=dY.device)
         _lib.call("ured_wgrad_skinny", _p(dY), int(ldd), _addr(X, X_off), int(ldx), int(Cout), int(Kin), int(Mrows),
-                  int(pro), _p(pro_s), _p(pro_t), _p(ws), _lib.stream_of(dY))
-        splitk_reduce(ws, nb, Cout, Kin, out, ldo, accumulate, out_off)
+                  int(pro), _p(pro_s), _p(pro_t), _addr(out, out_off), int(ldo), int(bool(accumulate)), _p(ws),
+                  _lib.stream_of(dY))
         return
     splits = choose_splits(Cout, Kin, Mrows)
     if splits == 1 and not accumulate:

@@ -198,11 +198,13 @@ typedef struct UredGemmDesc {
 int ured_gemm(const UredGemmDesc* d, void* stream);
 
 /* Weight gradient of an edge layer (min(Cout, Kin) <= 4, the other <= 256):
- * ws[blk][co][ki] = sum_{m in block blk} dY[m*ldd + co] * pro(X[m*ldx + ki]) for blocks of 256
- * rows (ceil(M/256) of them); finish with ured_splitk_reduce(ws, ceil(M/256), Cout, Kin, ...).
- * Replaces the MFMA wgrad for the 3-channel layers (a 128x128 tile would be almost all padding). */
+ * out[co*ldo + ki] (+)= sum_m dY[m*ldd + co] * pro(X[m*ldx + ki]), deterministic (row-block
+ * partials in ws, then a fixed-order tree per output). ws holds URED_SKINNY_WS_BLOCKS*Cout*Kin
+ * floats. Replaces the MFMA wgrad for the 3-channel layers (a 128x128 tile would be mostly padding). */
+#define URED_SKINNY_WS_BLOCKS 256
 int ured_wgrad_skinny(const float* dY, int ldd, const float* X, int ldx, int Cout, int Kin, int M, int pro,
-                      const float* pro_s, const float* pro_t, float* ws, void* stream);
+                      const float* pro_s, const float* pro_t, float* out, int ldo, int accumulate, float* ws,
+                      void* stream);
 
 /* Sum split-K partials: out[m][n] = (accumulate ? out : 0) + sum_z ws[z][m][n] (+ bias[n] if non-NULL);
  * fixed combine order (deterministic). */

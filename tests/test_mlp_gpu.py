@@ -28,7 +28,8 @@ def K(dev):
     return kernels
 
 
-@pytest.mark.parametrize("M,N,Kd", [(1000, 70, 33), (128, 128, 32), (300, 3, 32), (257, 64, 3), (4096, 1024, 64)])
+@pytest.mark.parametrize("M,N,Kd", [(1000, 70, 33), (128, 128, 32), (300, 3, 32), (257, 64, 3), (4096, 1024, 64),
+                                   (5000, 64, 3)])
 def test_gemm_forward_store(K, dev, M, N, Kd):
     g = torch.Generator().manual_seed(M + N + Kd)
     A = torch.randn(M, Kd, generator=g)
@@ -76,6 +77,27 @@ def test_gemm_wgrad_and_dgrad(K, dev):
     dX = torch.empty(M, Kd, device=dev)
     K.gemm(M, Kd, N, dY.to(dev), N, W.to(dev), Kd, dX, Kd, b_kmajor=True)
     close(dX, dY @ W, 1e-5, "dgrad")
+
+
+def test_gemm_k3_padded_views(K, dev):
+    """The xyz-layer GEMMs (K = 3, zero-padded to 4 for the MFMA kernel) on strided, offset views:
+    forward with batch statistics, and the k-major dgrad form."""
+    g = torch.Generator().manual_seed(33)
+    M, N = 9000, 96
+    A = torch.randn(M, 8, generator=g)
+    W = torch.randn(N, 7, generator=g)
+    Y = torch.empty(M, N, device=dev)
+    ws = torch.empty(K.nblocks(M), 2, N, device=dev)
+    K.gemm(M, N, 3, A.to(dev), 8, W.to(dev), 7, Y, N, A_off=2, B_off=1, epi=K.EPI_FWD, stat_ws=ws)
+    ref = A[:, 2:5] @ W[:, 1:4].t()
+    close(Y, ref, 1e-5, "k3 fwd")
+    st = K.bn_fwd_finalize(ws, M, N, torch.ones(N, device=dev), torch.zeros(N, device=dev), 1e-5, 0.1,
+                           torch.zeros(N, device=dev), torch.ones(N, device=dev))
+    close(st.mean, ref.double().mean(0).float(), 1e-5, "k3 fwd mean")
+    Wk = torch.randn(5, N + 4, generator=g)
+    dX = torch.empty(M, N, device=dev)
+    K.gemm(M, N, 3, A.to(dev), 8, Wk.to(dev), N + 4, dX, N, A_off=2, B_off=N + 4 + 2, b_kmajor=True)
+    close(dX, A[:, 2:5] @ Wk[1:4, 2:2 + N], 1e-5, "k3 dgrad")
 
 
 CFG = {"source_latent_dim": 64, "target_latent_dim": 64, "sem_latent_dim": 16, "MAX_NUM_PARTS": 16}
@@ -221,12 +243,15 @@ def test_residual_net_plain_forward(dev):
 
 
 @pytest.mark.parametrize("Cout,Kin,pro,M", [(3, 32, 0, 70001), (64, 3, 0, 4099), (3, 64, 1, 20000),
-                                            (3, 128, 2, 513), (256, 4, 0, 255), (5, 3, 1, 1000)])
+                                            (3, 128, 2, 513), (256, 4, 0, 255), (5, 3, 1, 1000),
+                                            (2, 64, 0, 100), (64, 1, 1, 37), (4, 96, 2, 1), (3, 32, 0, 0)])
 def test_wgrad_skinny_edge_layers(K, dev, Cout, Kin, pro, M):
     """The 3-channel edge layers' weight gradients (ured_wgrad_skinny): strided dY/X views,
     a column offset into X, the encoder prologues, accumulate into an existing gradient."""
     g = torch.Generator().manual_seed(Cout * 1000 + Kin + pro)
     ldd, ldx, xoff = Cout + 5, Kin + 7, 3
+    if M % 2:                                   # also the aligned float4 path
+        ldd, ldx, xoff = Cout, Kin, 0
     dY = torch.randn(M, ldd, generator=g)
     X = torch.randn(M, ldx, generator=g)
     s, t = torch.rand(Kin, generator=g) + 0.5, torch.randn(Kin, generator=g)
