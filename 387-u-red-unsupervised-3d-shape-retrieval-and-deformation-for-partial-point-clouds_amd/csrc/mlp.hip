@@ -630,7 +630,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
 // ---- v2: LDS-DMA staged, persistent kernel (all-VEC shapes) ---------------------
 // Both operands reach LDS by buffer_load_dwordx4 ... lds (no VGPR round trip, no staging
 // registers): a row-major [rows][k] operand lands as a [128][32] image with its 16-B
-// slots XOR-swizzled by (row & 7) and is read 4 consecutive k per ds_read_b128; a k-major
+// slots XOR-swizzled by ((row >> 1) & 7) and is read 4 consecutive k per ds_read_b128 (that
+// swizzle keeps each of ds_read_b128's four 16-lane bank groups, lanes {0-3,12-15,20-27},
+// {4-11,16-19,28-31} and their +32 twins, on 16 distinct 16-B slots: conflict-free; the
+// plain (row & 7) swizzle put two lanes of a group on one slot); a k-major
 // [k][cols] operand lands as a plain [32][128] image and is read with ds_read_b32.
 // The MFMA k-order is permuted (k-step j of lane half h uses k = 16h + j) so both image
 // kinds feed the same 32x32x2 sequence. The previous layer's BatchNorm+ReLU prologue is
@@ -642,7 +645,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 
 // 1024 16-B chunks per 128x32 operand image; wave w issues chunks [w*256, w*256+256) as 4
 // buffer-descriptor DMAs (operands < 2 GiB). Row-major: chunk c = (row r = c>>3, slot
-// p = c&7) reads k = 4*(p ^ (r&7)) (the XOR swizzle is on the source address, the LDS image
+// p = c&7) reads k = 4*(p ^ ((r>>1)&7)) (the XOR swizzle is on the source address, the LDS image
 // stays lane-linear); k-major: chunk c = (k = c>>5, 4 columns at 4*(c&31)). The per-lane
 // byte offsets are computed once per tile; a K-step only adds its k offset. Lanes whose row (row-major) or
 // column (k-major) is outside the operand get an offset past num_records, and so does any
@@ -692,7 +695,7 @@ __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld,
     for (int i = 0; i < 4; ++i) {
         const int c = (w * 4 + i) * 64 + lane;
         if constexpr (!KM) {
-            const int r = c >> 3, p = c & 7, sl = p ^ (r & 7);
+            const int r = c >> 3, p = c & 7, sl = p ^ ((r >> 1) & 7);
             const int row = e0 + r;
             o.vo[i] = row < ext ? (unsigned)(((long long)row * ld + 4 * sl) * 4) : BUF_OOB;
         } else {
@@ -878,7 +881,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                     const int r = wm * 64 + tm * 32 + li;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const float4 v4 = *reinterpret_cast<const float4*>(As + r * 32 + 4 * ((4 * h + q) ^ (r & 7)));
+                        const float4 v4 = *reinterpret_cast<const float4*>(As + r * 32 + 4 * ((4 * h + q) ^ ((r >> 1) & 7)));
                         a[tm][4 * q] = v4.x; a[tm][4 * q + 1] = v4.y; a[tm][4 * q + 2] = v4.z; a[tm][4 * q + 3] = v4.w;
                     }
                 }
@@ -894,7 +897,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                 if constexpr (!B_KM) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const float4 v4 = *reinterpret_cast<const float4*>(Bs + cidx * 32 + 4 * ((4 * h + q) ^ (cidx & 7)));
+                        const float4 v4 = *reinterpret_cast<const float4*>(Bs + cidx * 32 + 4 * ((4 * h + q) ^ ((cidx >> 1) & 7)));
                         b[tn][4 * q] = v4.x; b[tn][4 * q + 1] = v4.y; b[tn][4 * q + 2] = v4.z; b[tn][4 * q + 3] = v4.w;
                     }
                 } else {
