@@ -4,6 +4,7 @@ Every wrapper launches on torch's current stream of the output's device and
 raises on a non-zero status. Activations are point-major [M][C] fp32 tensors.
 """
 import ctypes
+import os
 
 import torch
 
@@ -212,13 +213,18 @@ def splitk_reduce(ws, splits, M, N, out, ldo, accumulate=False, out_off=0, bias=
               int(bool(accumulate)), _p(bias), _lib.stream_of(out))
 
 
+_WGRAD_WGS = int(os.environ.get("URED_WGRAD_WGS", "512"))        # tuning knobs (bench sweeps)
+_WGRAD_MIN_K = int(os.environ.get("URED_WGRAD_MIN_K", "512"))
+
+
 def choose_splits(Mo, No, K):
-    """Split-K factor of a weight gradient (K = points): about 1024 workgroups in total, at
+    """Split-K factor of a weight gradient (K = points): about 512 workgroups in total (one
+    resident round of 2 blocks per CU; 1024/1536/2048 measured 0.4-1.2% slower per step), at
     least 512 points per split (128 for outputs of <= 4 tiles, whose few workgroups would
     otherwise each walk hundreds of K-steps), at most 256 splits."""
     tiles = ((Mo + 127) // 128) * ((No + 127) // 128)
-    min_k = 128 if tiles <= 4 else 512
-    s = max(1, min(1024 // max(tiles, 1), K // min_k))
+    min_k = 128 if tiles <= 4 else _WGRAD_MIN_K
+    s = max(1, min(_WGRAD_WGS // max(tiles, 1), K // min_k))
     return max(1, min(s, 256))
 
 
