@@ -1363,14 +1363,17 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const float* __restrict__ Y
     }
 }
 
-// out[g][n] = sum of rows [r0, r1) of column n. Block = 4 waves x 64 columns; wave w sums
-// rows r0+w, r0+w+4, ... with four independent accumulators (16 rows in flight per lane; a
-// wave reads 256 contiguous bytes per row), combined in a fixed order and across waves in
-// LDS: deterministic. blockIdx.z = split s of S: the group's rows are cut into S equal
-// ranges and split s writes ws[g][s][n] (S > 1) for a second pass over the S partials.
-__global__ __launch_bounds__(256) void group_colsum_kernel(const float* __restrict__ X, int ldx, int N,
+// out[g][n] = sum of rows [r0, r1) of column n. Block = 16 waves x 64 columns; wave w sums
+// rows r0+w, r0+w+16, ... with eight independent accumulators (a wave reads 256 contiguous
+// bytes per row, 8 rows in flight per lane, 128 per column), combined in a fixed order and
+// across waves in LDS: deterministic. The short sums here (the per-128-row partials of a
+// BN backward, 256-512 rows) are latency chains, hence the width. blockIdx.z = split s of S:
+// the group's rows are cut into S equal ranges and split s writes ws[g][s][n] (S > 1) for a
+// second pass over the S partials.
+constexpr int GCS_WAVES = 16;
+__global__ __launch_bounds__(GCS_WAVES * 64) void group_colsum_kernel(const float* __restrict__ X, int ldx, int N,
         const int* __restrict__ off, int group_rows, float* __restrict__ out, int ldo) {
-    __shared__ float part[4][64];
+    __shared__ float part[GCS_WAVES][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int n = blockIdx.x * 64 + lane;
     const int g = blockIdx.y, S = gridDim.z, sp = blockIdx.z;
@@ -1378,22 +1381,24 @@ __global__ __launch_bounds__(256) void group_colsum_kernel(const float* __restri
     const int g1 = off ? off[g + 1] : (g + 1) * group_rows;
     const long long len = g1 - g0;
     const int r0 = g0 + (int)(len * sp / S), r1 = g0 + (int)(len * (sp + 1) / S);
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (n < N) {
         const float* col = X + n;
         int r = r0 + w;
-        for (; r + 12 < r1; r += 16) {
-            a0 += col[(size_t)r * ldx];
-            a1 += col[(size_t)(r + 4) * ldx];
-            a2 += col[(size_t)(r + 8) * ldx];
-            a3 += col[(size_t)(r + 12) * ldx];
+        for (; r + 7 * GCS_WAVES < r1; r += 8 * GCS_WAVES) {
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = col[(size_t)(r + i * GCS_WAVES) * ldx];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] += v[i];
         }
-        for (; r < r1; r += 4) a0 += col[(size_t)r * ldx];
+        for (; r < r1; r += GCS_WAVES) a[0] += col[(size_t)r * ldx];
     }
-    part[w][lane] = (a0 + a1) + (a2 + a3);
+    part[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     __syncthreads();
     if (w == 0 && n < N) {
-        const float v = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+        float v = part[0][lane];
+        for (int q = 1; q < GCS_WAVES; ++q) v += part[q][lane];
         if (S == 1) out[(size_t)g * ldo + n] = v;
         else out[((size_t)g * S + sp) * N + n] = v;
     }
@@ -1684,11 +1689,11 @@ int ured_group_colsum_split(const float* X, int ldx, int N, const int* off, int 
     URED_REQUIRE(splits == 1 || ws, "ured_group_colsum: splits > 1 needs a workspace [G][splits][N]");
     URED_REQUIRE(G <= 65535, "ured_group_colsum: G=%d > 65535", G);
     dim3 grid((N + 63) / 64, G, splits);
-    hipLaunchKernelGGL(group_colsum_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, ldx, N, off, group_rows,
+    hipLaunchKernelGGL(group_colsum_kernel, grid, dim3(GCS_WAVES * 64), 0, (hipStream_t)stream, X, ldx, N, off, group_rows,
                        splits == 1 ? out : ws, ldo);
     if (splits > 1) {   // second pass: the S partials of each group, in split order
         dim3 grid2((N + 63) / 64, G, 1);
-        hipLaunchKernelGGL(group_colsum_kernel, grid2, dim3(256), 0, (hipStream_t)stream, ws, N, N, nullptr, splits,
+        hipLaunchKernelGGL(group_colsum_kernel, grid2, dim3(GCS_WAVES * 64), 0, (hipStream_t)stream, ws, N, N, nullptr, splits,
                            out, ldo);
     }
     return ured::launch_status("ured_group_colsum");

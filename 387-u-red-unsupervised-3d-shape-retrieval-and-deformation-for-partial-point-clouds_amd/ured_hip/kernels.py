@@ -58,6 +58,9 @@ def nblocks(M):
     return (M + BM - 1) // BM
 
 
+_SHAPE_LOG = [] if os.environ.get("URED_GEMM_SHAPES") else None    # diagnostics: every launch's shape
+
+
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro_a=PRO_NONE, pro_b=PRO_NONE,
          epi=EPI_STORE, A_off=0, B_off=0, C_off=0, A2=None, lda2=0, k1=None, pro_s=None, pro_t=None, bias=None,
          rowbias=None, ldr=0, gidx=None, group_rows=0, stat_relu=False, stat_ws=None, pool_ws=None,
@@ -75,6 +78,8 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro
                  A_off=A_off, B_off=B_off)
             splitk_reduce(ws, sp, M, N, C, ldc, False, C_off, bias=bias)
             return
+    if _SHAPE_LOG is not None:
+        _SHAPE_LOG.append((int(M), int(N), int(K), bool(a_kmajor), bool(b_kmajor), pro_a, pro_b, epi, int(splits)))
     d = GemmDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
     d.a_kmajor, d.b_kmajor, d.pro_a, d.pro_b, d.epi = int(a_kmajor), int(b_kmajor), pro_a, pro_b, epi
@@ -191,7 +196,7 @@ def group_colsum(X, N, G, *, off=None, group_rows=0, ldx=None, out=None, rows=No
     per = max(1, rows // max(G, 1))
     blocks = ((N + 63) // 64) * G
     splits = 1
-    while per // (splits * 2) >= 256 and blocks * splits < 2048 and splits < 256:
+    while per // (splits * 2) >= 1024 and blocks * splits < 1024 and splits < 256:
         splits *= 2
     ws = torch.empty(G, splits, N, device=X.device) if splits > 1 else None
     _lib.call("ured_group_colsum_split", _p(X), int(N if ldx is None else ldx), int(N), _p(off), int(group_rows),
