@@ -973,31 +973,36 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
 
 // ---- small kernels -------------------------------------------------------------
 
-// out[m][n] (+)= sum_z ws[z][m][n]. Block = 64 consecutive elements x 4 waves; wave w sums
-// splits w, w+4, ... with four independent accumulators; fixed combine order (deterministic).
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
-                                                            float* __restrict__ out, int ldo, int accumulate,
-                                                            const float* __restrict__ bias) {
-    __shared__ float part[4][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// out[m][n] (+)= sum_z ws[z][m][n]. Block = 64 consecutive elements x nw waves (nw = blockDim/64,
+// up to 16, chosen by the launcher from the split count); wave w sums splits w, w+nw, ... with
+// eight loads in flight; fixed combine order (deterministic). Many of these reductions are
+// short (a few thousand outputs over 8-128 splits): latency chains, hence the width.
+__global__ __launch_bounds__(1024) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                             float* __restrict__ out, int ldo, int accumulate,
+                                                             const float* __restrict__ bias) {
+    __shared__ float part[16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const size_t total = (size_t)M * N;
     const size_t e = (size_t)blockIdx.x * 64 + lane;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (e < total) {
         int z = w;
-        for (; z + 12 < splits; z += 16) {
-            a0 += ws[(size_t)z * total + e];
-            a1 += ws[(size_t)(z + 4) * total + e];
-            a2 += ws[(size_t)(z + 8) * total + e];
-            a3 += ws[(size_t)(z + 12) * total + e];
+        for (; z + 7 * nw < splits; z += 8 * nw) {
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = ws[(size_t)(z + i * nw) * total + e];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] += v[i];
         }
-        for (; z < splits; z += 4) a0 += ws[(size_t)z * total + e];
+        for (; z < splits; z += nw) a[0] += ws[(size_t)z * total + e];
     }
-    part[w][lane] = (a0 + a1) + (a2 + a3);
+    part[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     __syncthreads();
     if (w == 0 && e < total) {
         const int m = (int)(e / N), n = (int)(e % N);
-        const float sum = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]) + (bias ? bias[n] : 0.f);
+        float sum = part[0][lane];
+        for (int q = 1; q < nw; ++q) sum += part[q][lane];
+        if (bias) sum += bias[n];
         float* o = out + (size_t)m * ldo + n;
         *o = accumulate ? *o + sum : sum;
     }
@@ -1577,7 +1582,9 @@ int ured_splitk_reduce(const float* ws, int splits, int M, int N, float* out, in
     URED_REQUIRE(ws && out, "ured_splitk_reduce: null pointer");
     const size_t total = (size_t)M * N;
     URED_REQUIRE((total + 63) / 64 <= 0x7fffffff, "ured_splitk_reduce: too many elements");
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
+    int nw = 1;
+    while (nw < 16 && nw * 8 < splits) nw *= 2;      // about 8 splits per wave
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + 63) / 64)), dim3(64 * nw), 0, (hipStream_t)stream,
                        ws, splits, M, N, out, ldo, accumulate, bias);
     return ured::launch_status("ured_splitk_reduce");
 }
