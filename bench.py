@@ -27,7 +27,10 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X fp32 (vector = matrix) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARY = "r1y_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
+PMC_SUMMARY = "r1z_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
+CLOCK_SUMMARY = "r1z_clock_summary.json"   # GRBM_GUI_ACTIVE pass (tools/gpu41.sh): clock held per kernel
+SQ_SUMMARY = "r1z_sq_summary.json"         # SQ pass (tools/gpu42.sh): MFMA-busy cycles per kernel
+NOMINAL_GHZ = 2.4
 
 
 def workload_cfg(args):
@@ -435,6 +438,21 @@ def main():
                     "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
                     "kernel": dom_key, "launches_per_step": round(lps, 2), "avg_launch_ms": round(avg_ms, 4),
                     "flop_per_launch": round(flop_per_launch), "timing": timing}
+        clk = os.path.join(ROOT, "profiles", CLOCK_SUMMARY)
+        if os.path.exists(clk):
+            for kname, v in json.load(open(clk)).items():
+                if dom_key in kname:
+                    # the chip holds ~2.2 GHz under this MFMA load (DVFS): the peak at that clock
+                    ghz = v["effective_ghz"]
+                    roofline["held_clock_ghz"] = round(ghz, 3)
+                    roofline["frac_at_held_clock"] = round(ach / (PEAK_FP32_TFLOPS * ghz / NOMINAL_GHZ), 4)
+                    roofline["clock_source"] = os.path.relpath(clk, ROOT)
+        sq = os.path.join(ROOT, "profiles", SQ_SUMMARY)
+        if os.path.exists(sq):
+            for kname, v in json.load(open(sq)).items():
+                if dom_key in kname and v.get("GRBM_GUI_ACTIVE"):
+                    # SQ_VALU_MFMA_BUSY_CYCLES over the 1024 SIMDs x the kernel's cycles
+                    roofline["mfma_busy"] = round(v["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * v["GRBM_GUI_ACTIVE"] / 8), 4)
         if "attainable_ms" in d:
             # the same launches against the per-launch roofline min(MFMA peak, AI x HBM peak): the
             # small-K shapes of this kernel sit near the ridge (AI ~ 20-40 FLOP/B)
