@@ -198,6 +198,35 @@ def chamfer_rate(dev, B=16, n=2048, m=2048, iters=20):
             "hbm_read_frac": round(12 * B * (n + m) / t / 8e12, 6)}
 
 
+def chamfer_published_cmp(dev, iters=50):
+    """BASELINE.md §1's only published hot-path number: chamfer3D forward+backward on
+    p1 = 32x2000x3, p2 = 32x1000x3 in 1.4 ms (ChamferDistancePytorch/README.md:48-56, GPU model
+    unstated). Same call through our drop-in chamfer_3DDist (allocation, both directions, the
+    gradient of d1.mean() + d2.mean())."""
+    from chamfer3D.dist_chamfer_3D import chamfer_3DDist
+    cd = chamfer_3DDist()
+    g = torch.Generator().manual_seed(0)
+    p1 = torch.rand(32, 2000, 3, generator=g).to(dev).requires_grad_(True)
+    p2 = torch.rand(32, 1000, 3, generator=g).to(dev).requires_grad_(True)
+
+    def once():
+        d1, d2, _, _ = cd(p1, p2)
+        (d1.mean() + d2.mean()).backward()
+    for _ in range(5):
+        once()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        once()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / iters
+    return {"shape": "32x2000x1000", "fwd_bwd_ms": round(t, 4), "gpair_s": round(32 * 2000 * 1000 / (t * 1e-3) / 1e9, 1),
+            "published_ms": 1.4, "published_source": "ChamferDistancePytorch/README.md:48-56 (GPU unstated)",
+            "speedup_vs_published": round(1.4 / t, 2)}
+
+
 def emd_rate(dev, B=16, n=2048, eps=0.005, iters=50, reps=5):
     """§8(f)4: calc_emd's default auction (eps 0.005, 50 rounds, utils_v2/model_utils.py:72) on
     16 x 2048-point clouds: ms per call and the fraction of points matched one-to-one."""
@@ -221,7 +250,7 @@ def emd_rate(dev, B=16, n=2048, eps=0.005, iters=50, reps=5):
             "bijective_fraction": round(uniq, 4), "emd": round(float(torch.sqrt(dist).mean()), 6)}
 
 
-def inference_rate(cfg, db, dev, iters=10):
+def inference_rate(cfg, db, dev, iters=30, reps=2):
     """Config 3 (table, bs=16, 2048 pts): the engine/test.py retrieval + deformation inference
     path — encode the source DB once (eval BN, chunks of 512), then per batch: target encoder,
     part pooling, cosine retrieval over the DB, DeformNet, get_shape, chamfer."""
@@ -237,14 +266,19 @@ def inference_rate(cfg, db, dev, iters=10):
     codes = encode_sources(models, db)
     torch.cuda.synchronize()
     t_db = time.perf_counter() - t0
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        infer(models, db, b, cfg, codes)
-    e1.record()
-    torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / iters * 1e-3
+    # host-launch-bound (many small kernels per batch): best of `reps` timed runs
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            infer(models, db, b, cfg, codes)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / iters * 1e-3)
+    t = min(ts)
     return {"workload": "config 3: engine/test.py inference, bs=16, 2048 pts, 4 parts/target",
+            "runs_ms_per_batch": [round(x * 1e3, 3) for x in ts],
             "batches_per_s": round(1.0 / t, 2), "targets_per_s": round(16.0 / t, 1), "ms_per_batch": round(t * 1e3, 3),
             "source_db_encode_ms": round(t_db * 1e3, 3), "sources": int(db.num_sources)}
 
@@ -475,6 +509,7 @@ def main():
         extra["chamfer_gpair_s"] = ch["gpair_dist_s"]
         extra["chamfer"] = [ch, chamfer_rate(dev, 64, 4096, 4096, iters=10),
                             chamfer_rate(dev, 16, 16384, 2048, iters=10)]
+        extra["chamfer_vs_published"] = chamfer_published_cmp(dev)
         extra["pseudo_label_dcd"] = pair_rate(dev)
         extra["inference"] = inference_rate(cfg, db, dev)
         extra["emd"] = emd_rate(dev)
