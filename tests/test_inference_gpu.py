@@ -94,3 +94,26 @@ def test_inference_scores_and_meshes(dev):
             A = mesh["vmats"][mesh["voff"][s]:mesh["voff"][s + 1]]
             exp = get_shape_numpy(A, params[bb, i].reshape(1, 6, 1), pdef[bb, i].reshape(6, 1), 0.1).reshape(-1, 3)
             np.testing.assert_allclose(v[off[bb * 16 + i]:off[bb * 16 + i + 1]], exp, rtol=1e-5, atol=1e-6)
+
+
+def test_graphed_inference_matches_eager(dev):
+    """GraphedInfer (one HIP graph per batch shape) replays bit-identically to infer() for new
+    batches of the captured shape."""
+    from dataset import synthetic
+    from train_utils.load_sources import SourceDB
+    from engine.train import get_models, batch_to_device
+    from engine.test import encode_sources, infer, GraphedInfer
+    ns = 400
+    dbn = synthetic.make_source_db(ns, seed=31)
+    db = SourceDB(dbn["src_points"], dbn["src_mats"], dbn["src_default_param"], dbn["src_sem"], dev)
+    models, _, _ = get_models(CFG, dev)
+    codes = encode_sources(models, db)
+    gi = GraphedInfer(models, db, CFG, codes)
+    batches = [batch_to_device(synthetic.make_batch(3, 256, ns, parts=[4, 2, 7], seed=40 + i), dev)
+               for i in range(3)]
+    for i, b in enumerate(batches):
+        got = gi(b)                               # first call: eager + capture; then replays
+        ref = infer(models, db, b, CFG, codes)
+        for k in ("retrieved", "params", "out", "cd", "re_score", "sim_top2_gap"):
+            assert torch.equal(got[k], ref[k]), (i, k)
+    assert len(gi.graphs) == 1
