@@ -64,6 +64,23 @@ def allreduce_gradients(buckets, world, stream=None):
             flat.record_stream(main)
 
 
+def allreduce_flat(flat, world, bucket_elems, stream=None):
+    """Average a flat gradient buffer over the process group: all_reduce on ~bucket_elems views
+    of it in place (no gather/scatter copies), all issued before the first wait."""
+    main = torch.cuda.current_stream() if stream is not None else None
+    if stream is not None:
+        stream.wait_stream(main)
+    ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
+    with ctx:
+        works = [dist.all_reduce(flat[o:o + bucket_elems], op=dist.ReduceOp.SUM, async_op=True)
+                 for o in range(0, flat.numel(), bucket_elems)]
+    for w in works:
+        w.wait()
+    if stream is not None:
+        main.wait_stream(stream)
+    flat.mul_(1.0 / world)
+
+
 class _nullctx:
     def __enter__(self):
         return self
@@ -87,6 +104,11 @@ class DataParallelStep(TrainStep):
 
     def reduce_gradients(self):
         if self.world == 1:
+            return
+        if getattr(self.optimizer, "flat_param", None) is not None:
+            # FlatAdam: gather the gradients into its flat buffer once, all-reduce that in place
+            self.optimizer.gather_grads()
+            allreduce_flat(self.optimizer.flat_grad, self.world, self.bucket_elems, self.comm_stream)
             return
         if self._buckets is None:           # first step: learn which parameters receive gradients
             self._buckets = make_buckets(self.params, self.bucket_elems)

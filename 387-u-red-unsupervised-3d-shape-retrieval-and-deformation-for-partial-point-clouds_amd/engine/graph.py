@@ -119,5 +119,8 @@ class GraphedStep:
             v.copy_(batch[name], non_blocking=True)
         g.replay()
         self.inner.reduce_gradients()
+        sync = getattr(self.inner.optimizer, "sync_lr", None)
+        if sync is not None:                 # FlatAdam reads lr from a device scalar
+            sync()
         self.g_update.replay()
         return T

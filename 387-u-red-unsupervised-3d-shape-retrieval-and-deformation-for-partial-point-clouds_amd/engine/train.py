@@ -256,6 +256,9 @@ class TrainStep:
         (engine/train.py:331-336) with the per-tensor norms of all six in one multi-tensor
         launch and the six totals / clip factors as one small vector (deterministic: fixed-order
         row sums, no atomics); then Adam."""
+        if hasattr(self.optimizer, "flat_grad"):      # FlatAdam (ured_hip/optim.py): one fused tail
+            self.optimizer.step(max_norm=max_norm)
+            return
         groups = [[p.grad for p in self.models[name].parameters() if p.grad is not None] for name in CLIPPED]
         grads = [g for grp in groups for g in grp]
         if grads:

@@ -12,6 +12,13 @@ def define_optimizer_dm_re_recon(target_encoder_full, param_decoder_full, recon_
     if cfg["optimizer"] == "sgd":
         opt = torch.optim.SGD(params, lr=cfg["learning_rate"], momentum=cfg["momentum"],
                               weight_decay=cfg["weight_decay"])
+    elif cfg["optimizer"] == "adam" and params and params[0].is_cuda and cfg.get("flat_adam", True):
+        # the same Adam (and the six clip_grad_norm_ calls, TrainStep.clip_and_step) over flat
+        # HBM buffers: ured_hip/optim.py
+        from ured_hip.optim import FlatAdam
+        mods = (target_encoder_full, param_decoder_full, re_net_full, recon_full, src_encoder, recon_src)
+        opt = FlatAdam(params, [list(m.parameters()) for m in mods], lr=cfg["learning_rate"],
+                       betas=(0.9, 0.999), eps=1e-8, weight_decay=cfg["weight_decay"])
     elif cfg["optimizer"] == "adam":
         kw = {}
         if params and params[0].is_cuda and cfg.get("fused_adam", True):

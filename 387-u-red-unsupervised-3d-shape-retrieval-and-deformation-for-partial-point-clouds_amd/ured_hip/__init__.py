@@ -5,5 +5,6 @@
   kernels  typed wrappers of the fused per-point MLP entry points
   mlp      PointEncoderFn / ResidualNetFn autograd chains
   attn     graph-node multi-head attention (DeformNet's GraphAttentionNet core)
+  optim    FlatAdam: per-module gradient clipping + Adam over flat buffers
 """
-from . import _lib, attn, kernels, nn  # noqa: F401
+from . import _lib, attn, kernels, nn, optim  # noqa: F401

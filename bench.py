@@ -37,7 +37,8 @@ def workload_cfg(args):
     with open(os.path.join(ge.PKG_DIR, "config", "config_train_test.json")) as f:
         cfg = json.load(f)
     cfg.update({"batch_size": args.batch, "num_points": args.points, "parts": args.parts,
-                "num_source": args.sources, "device": "cuda", "log_every": 0})
+                "num_source": args.sources, "device": "cuda", "log_every": 0,
+                "flat_adam": os.environ.get("URED_FLAT_ADAM", "1") == "1"})   # A/B knob: torch's Adam
     return cfg
 
 

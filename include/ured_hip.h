@@ -197,6 +197,20 @@ typedef struct UredGemmDesc {
 
 int ured_gemm(const UredGemmDesc* d, void* stream);
 
+/* Optimizer tail of the training step (reference engine/train.py:331-346: clip_grad_norm_(5.0)
+ * per module, then torch.optim.Adam with L2 weight decay, train_utils/optimizer_dm.py:68-104)
+ * over flat buffers param/grad/exp_avg/exp_avg_sq. Chunk c covers [chunk_beg[c], chunk_end[c])
+ * (16-B aligned, lengths multiples of 4) of module segment chunk_seg[c]; segment s owns chunks
+ * [seg_chunk0[s], seg_chunk0[s+1]). max_norm > 0: per-segment L2 norm (fp64 chunk partials in
+ * `partial`, fixed order) -> coef[s] = min(max_norm / (norm + 1e-6), 1), gradient scaled in
+ * place; max_norm <= 0: no clipping. *step (device) is incremented, then every element takes
+ * one Adam step with *lr (device). Deterministic. */
+int ured_adam_clip_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq,
+                        const long long* chunk_beg, const long long* chunk_end, const int* chunk_seg, int nchunks,
+                        const int* seg_chunk0, int nseg, float max_norm, const float* lr, float* step,
+                        double beta1, double beta2, double eps, double weight_decay, double* partial, float* coef,
+                        void* stream);
+
 /* Weight gradient of an edge layer (min(Cout, Kin) <= 4, the other <= 256):
  * out[co*ldo + ki] (+)= sum_m dY[m*ldd + co] * pro(X[m*ldx + ki]), deterministic (row-block
  * partials in ws, then a fixed-order tree per output). ws holds URED_SKINNY_WS_BLOCKS*Cout*Kin

@@ -25,14 +25,14 @@ CFG = {"source_latent_dim": 64, "target_latent_dim": 64, "sem_latent_dim": 16, "
        "weight_decay": 5e-4, "lr_stepsize": 3, "lr_decay": 0.5, "momentum": 0.9}
 
 
-def _setup(dev, B=2, N=128, parts=(3, 2), ns=24, seed=4, unique=True):
+def _setup(dev, B=2, N=128, parts=(3, 2), ns=24, seed=4, unique=True, **over):
     from dataset import synthetic
     from train_utils.load_sources import SourceDB
     from engine.train import TrainStep, batch_to_device
     db_np = synthetic.make_source_db(ns, seed=3)
     bt = synthetic.make_batch(B, N, ns, max_parts=16, parts=list(parts), seed=seed)
     db = SourceDB(db_np["src_points"], db_np["src_mats"], db_np["src_default_param"], db_np["src_sem"], dev)
-    cfg = dict(CFG, batch_size=B)
+    cfg = dict(CFG, batch_size=B, **over)
     ts = TrainStep(cfg, db, dev)
     P = ured_ref.make_params(cfg, seed=7)
     for name, sd in P.items():
@@ -147,11 +147,15 @@ def test_unique_sources_equal_all_slots(dev):
                 assert torch.equal(v, b2s[k])
 
 
-def test_fused_clip_matches_clip_grad_norm(dev):
-    """TrainStep.clip_and_step's one-launch clipping == torch.nn.utils.clip_grad_norm_ per module
-    (engine/train.py:331-336) up to fp32 rounding of the six module norms."""
+@pytest.mark.parametrize("flat", [True, False], ids=["flat_adam", "torch_adam"])
+def test_fused_clip_matches_clip_grad_norm(dev, flat):
+    """TrainStep.clip_and_step's clipping == torch.nn.utils.clip_grad_norm_ per module
+    (engine/train.py:331-336) up to fp32 rounding of the six module norms: the one-launch norm
+    path before torch's Adam, and FlatAdam's fused tail (the gradients it leaves are the clipped
+    ones)."""
     from engine.train import CLIPPED
-    ts = _setup(dev)[0]
+    ts = _setup(dev, flat_adam=flat)[0]
+    assert (type(ts.optimizer).__name__ == "FlatAdam") == flat
     for name in CLIPPED:                      # large gradients so that every module is clipped
         for p in ts.models[name].parameters():
             p.grad = torch.randn_like(p) * 10.0
@@ -162,11 +166,68 @@ def test_fused_clip_matches_clip_grad_norm(dev):
         coef = (5.0 / (total + 1e-6)).clamp(max=1.0)
         for g in gs:
             g.mul_(coef)
-    ts.optimizer.step = lambda: None          # clip only
+    if not flat:
+        ts.optimizer.step = lambda: None      # clip only
     ts.clip_and_step()
     for name in CLIPPED:
         for p, r in zip(ts.models[name].parameters(), ref[name]):
             torch.testing.assert_close(p.grad, r, rtol=2e-6, atol=1e-9)
+
+
+def test_flat_adam_matches_torch_adam(dev):
+    """FlatAdam (flat buffers, ured_adam_clip_step) == torch.optim.Adam(fused=True) with the same
+    L2 weight decay over several steps, gradients present on only some parameters (the others
+    untouched, as torch skips them), an lr change in between (StepLR's path), no clipping."""
+    from ured_hip.optim import FlatAdam
+    g = torch.Generator().manual_seed(3)
+    shapes = [(64, 3), (64,), (128, 64), (5,), (1024, 33), (7, 7)]
+    base = [torch.randn(*s, generator=g) for s in shapes]
+    pa = [torch.nn.Parameter(b.clone().to(dev)) for b in base]
+    pb = [torch.nn.Parameter(b.clone().to(dev)) for b in base]
+    fa = FlatAdam(pa, [pa[:3], pa[3:]], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=5e-4)
+    ta = torch.optim.Adam(pb, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=5e-4, fused=True)
+    live = [0, 1, 2, 4, 5]                    # parameter 3 never gets a gradient
+    for it in range(5):
+        if it == 3:
+            for o in (fa, ta):
+                o.param_groups[0]["lr"] = 5e-4
+        fa.zero_grad()
+        ta.zero_grad()
+        for i in live:
+            gr = torch.randn(*shapes[i], generator=g).to(dev)
+            pa[i].grad = gr.clone()
+            pb[i].grad = gr.clone()
+        fa.step()
+        ta.step()
+        for i in range(len(shapes)):
+            torch.testing.assert_close(pa[i].detach(), pb[i].detach(), rtol=1e-6, atol=1e-7, msg=f"step {it} p{i}")
+    assert torch.equal(pa[3].detach().cpu(), base[3])
+    assert fa.flat_grad is not None and pa[0].data_ptr() == fa.flat_param.data_ptr()
+
+
+def test_flat_adam_train_steps_match_torch_adam(dev):
+    """Full training steps with FlatAdam vs torch's Adam + the one-launch clip. After one step
+    the parameters agree to 1e-3 of the step's largest move (the clip factors differ in the last
+    bit: fp64 vs per-tensor fp32 norm sums; Adam's update is scale-free); over three steps the
+    losses agree to 1e-5 (later parameters drift apart by a few % of a move: the network
+    amplifies last-bit differences through Adam's normalised update)."""
+    ts1, batch = _setup(dev, flat_adam=True)[:2]
+    ts2 = _setup(dev, flat_adam=False)[0]
+    init = {name: {k: p.detach().clone() for k, p in m.named_parameters()} for name, m in ts2.models.items()}
+    for it in range(3):
+        T1, T2 = ts1.step(batch), ts2.step(batch)
+        a, b = T1["all_loss"].item(), T2["all_loss"].item()
+        assert abs(a - b) <= 1e-5 * abs(b) + 1e-7, (it, a, b)
+        if it > 0:
+            continue
+        for name, m in ts1.models.items():
+            p2 = dict(ts2.models[name].named_parameters())
+            move = max((p2[k].detach() - init[name][k]).abs().max().item() for k in p2)
+            for k, p in m.named_parameters():
+                if k in BN_FED_BIAS:
+                    continue      # exactly-zero true gradient: Adam's update of the noise is +-lr either way
+                d = (p.detach() - p2[k].detach()).abs().max().item()
+                assert d <= 1e-3 * move + 1e-9, (name, k, d, move)
 
 
 def test_bn_counters_count_steps(dev):
