@@ -201,6 +201,10 @@ __device__ __forceinline__ void store_kmajor(const RowTile& r, float* S) {
 
 template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; };
 
+#ifndef URED_BNBWD_YALL
+#define URED_BNBWD_YALL 1
+#endif
+
 // ---- shared epilogue ---------------------------------------------------------
 // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
 #define RED(a, q, c) red_f[((a) * 2 + (q)) * BN + (c)]
@@ -458,16 +462,20 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         // Yp one column half (32 values) at a time: the j = 0 half and the per-column
         // parameters are issued before pre() (the persistent kernel's next-tile DMA), the j = 1
         // half after the j = 0 half is processed (registers: acc 64 + one half 32)
-        f16v yh[2];
+        // URED_BNBWD_YALL: both halves (64 values) are issued at once instead — after the K-loop
+        // the fragment registers are dead, so the whole tile fits without raising the kernel's
+        // VGPR peak, and the epilogue then waits for one HBM round trip instead of two (gfx9
+        // vmcnt is in order: the second half's loads otherwise queue behind the first half's stores)
+        f16v yh[URED_BNBWD_YALL ? 2 : 1][2];
         InTile<BUFST> Yr(d.Yp, d.ldy, d.M, d.N);
         auto load_y = [&](int j) {
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) yh[i][r] = Yr.get(row_of(i, r), col);
+                for (int r = 0; r < 16; ++r) yh[URED_BNBWD_YALL ? j : 0][i][r] = Yr.get(row_of(i, r), col);
         };
-        load_y(0);
+        if (!URED_BNBWD_YALL) load_y(0);
         // max-pool backward: the pooled gradient lands on the winning row of each (group, column)
         const bool pool_blk = d.pool_idx && (d.pool_group_rows % BM == 0);
         const int pg = pool_blk ? m0 / d.pool_group_rows : 0;
@@ -482,11 +490,12 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             pidx_[j] = -1; pgr_[j] = 0.f;
             if (pool_blk && cv) { pidx_[j] = d.pool_idx[(size_t)pg * d.N + col]; pgr_[j] = d.pool_grad[(size_t)pg * d.N + col]; }
         }
+        if (URED_BNBWD_YALL) { load_y(0); load_y(1); }   // behind the (L2-resident) per-column parameters
         pre();
         OutTile<BUFST> Gw(d.C, d.ldc, d.M, d.N);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            if (j == 1) load_y(1);
+            if (!URED_BNBWD_YALL && j == 1) load_y(1);
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
             const bool cv = col < d.N;
             const float sc = sc_[j], sh = sh_[j], mu = mu_[j], is = is_[j];
@@ -507,7 +516,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                         if (d.pool_idx[ge] == row) dh += d.pool_grad[ge];
                     }
                     if (d.gadd && ok) dh += d.gadd[(size_t)row * d.ldg + col];
-                    const float y = yh[i][r];
+                    const float y = yh[URED_BNBWD_YALL ? j : 0][i][r];
                     float g, xh;
                     if (d.bwd_res == URED_ACT_RES) {
                         g = dh;
