@@ -61,6 +61,11 @@ def nblocks(M):
 _SHAPE_LOG = [] if os.environ.get("URED_GEMM_SHAPES") else None    # diagnostics: every launch's shape
 
 
+# K slice per split of the few-tile store GEMMs (the per-sample fc layers, M = batch): the
+# per-split K-loop is a chain of dependent DMA round trips, so shorter slices = more workgroups
+_SPLITK_KMIN = int(os.environ.get("URED_SPLITK_KMIN", "32"))
+
+
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro_a=PRO_NONE, pro_b=PRO_NONE,
          epi=EPI_STORE, A_off=0, B_off=0, C_off=0, A2=None, lda2=0, k1=None, pro_s=None, pro_t=None, bias=None,
          rowbias=None, ldr=0, gidx=None, group_rows=0, stat_relu=False, stat_ws=None, pool_ws=None,
@@ -72,7 +77,7 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro
             and K >= 512):
         tiles = ((M + BM - 1) // BM) * ((N + BM - 1) // BM)
         if tiles <= 16:
-            sp = min(1024 // tiles, K // 128)
+            sp = min(1024 // tiles, K // _SPLITK_KMIN)
             ws = torch.empty(sp, M, N, device=C.device)
             gemm(M, N, K, A, lda, B, ldb, ws, N, b_kmajor=b_kmajor, epi=EPI_SPLITK, splits=sp,
                  A_off=A_off, B_off=B_off)
