@@ -225,6 +225,9 @@ def splitk_reduce(ws, splits, M, N, out, ldo, accumulate=False, out_off=0, bias=
 
 _WGRAD_WGS = int(os.environ.get("URED_WGRAD_WGS", "512"))        # tuning knobs (bench sweeps)
 _WGRAD_MIN_K = int(os.environ.get("URED_WGRAD_MIN_K", "512"))
+_WGRAD_FEW_MIN_K = int(os.environ.get("URED_WGRAD_FEW_MIN_K", "128"))
+_WGRAD_FEW_WGS = int(os.environ.get("URED_WGRAD_FEW_WGS", "512"))
+_WGRAD_FEW_MAX = int(os.environ.get("URED_WGRAD_FEW_MAX", "256"))
 
 
 def choose_splits(Mo, No, K):
@@ -233,9 +236,10 @@ def choose_splits(Mo, No, K):
     least 512 points per split (128 for outputs of <= 4 tiles, whose few workgroups would
     otherwise each walk hundreds of K-steps), at most 256 splits."""
     tiles = ((Mo + 127) // 128) * ((No + 127) // 128)
-    min_k = 128 if tiles <= 4 else _WGRAD_MIN_K
-    s = max(1, min(_WGRAD_WGS // max(tiles, 1), K // min_k))
-    return max(1, min(s, 256))
+    few = tiles <= 4
+    min_k = _WGRAD_FEW_MIN_K if few else _WGRAD_MIN_K
+    s = max(1, min((_WGRAD_FEW_WGS if few else _WGRAD_WGS) // max(tiles, 1), K // min_k))
+    return max(1, min(s, _WGRAD_FEW_MAX if few else 256))
 
 
 def wgrad(dY, ldd, X, ldx, Cout, Kin, Mrows, out, ldo, *, out_off=0, X_off=0, pro=PRO_NONE, pro_s=None,
