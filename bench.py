@@ -27,7 +27,7 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X fp32 (vector = matrix) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARY = "r1f_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
+PMC_SUMMARY = "r1g_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
 CLOCK_SUMMARY = "r1z_clock_summary.json"   # GRBM_GUI_ACTIVE pass (tools/gpu41.sh): clock held per kernel
 SQ_SUMMARY = "r1z_sq_summary.json"         # SQ pass (tools/gpu42.sh): MFMA-busy cycles per kernel
 NOMINAL_GHZ = 2.4
