@@ -201,6 +201,9 @@ __device__ __forceinline__ void store_kmajor(const RowTile& r, float* S) {
 
 template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; };
 
+#ifndef URED_DGRAD_SMALL
+#define URED_DGRAD_SMALL 1
+#endif
 #ifndef URED_BNBWD_YALL
 #define URED_BNBWD_YALL 1
 #endif
@@ -1461,8 +1464,162 @@ int persist_slots() {
     return slots;
 }
 
+// 256 threads per 128-row block (1024 measured no faster and changes the summation order)
+constexpr int SMALL_NT = 256;
+
+// ---- edge-layer dgrad + BN-backward (K <= 4: the 3-channel output layers' input gradient) ----
+// dh[m][c] = sum_k dY[m][k] W[k][c] (+ gadd), then the EPI_BNBWD arithmetic of epilogue()
+// (ReLU/BN mask, G store, per-128-row-block partials {sum g, sum g*xhat} in bwd_ws), as a
+// streaming kernel: a 128x128 MFMA tile is ~all padding at K = 3 and N = 32/64. One block per
+// 128-row block (the partial layout the finalize expects); SMALL_NT / N row groups x N columns; each
+// thread keeps its W column in registers and walks its rows; fixed-order LDS combine.
+template <int KS>
+__global__ __launch_bounds__(SMALL_NT) void dgrad_small_bnbwd_kernel(const UredGemmDesc d) {
+    __shared__ float red[2][SMALL_NT];
+    const int N = d.N, rg = SMALL_NT / N, t = threadIdx.x;
+    const int c = t % N, g0 = t / N;
+    const int m0 = blockIdx.x * BM;
+    const int mend = min(m0 + BM, d.M);
+    float a1 = 0.f, a2 = 0.f;
+    if (g0 < rg) {
+        float w[KS];
+#pragma unroll
+        for (int k = 0; k < KS; ++k) w[k] = d.B[(size_t)k * d.ldb + c];
+        const float sc = d.bn_scale[c], sh = d.bn_shift[c], mu = d.bn_mean[c], is = d.bn_invstd[c];
+#pragma unroll 4
+        for (int m = m0 + g0; m < mend; m += rg) {
+            const float* a = d.A + (size_t)m * d.lda;
+            float dh = 0.f;
+#pragma unroll
+            for (int k = 0; k < KS; ++k) dh = __builtin_fmaf(a[k], w[k], dh);
+            if (d.gadd) dh += d.gadd[(size_t)m * d.ldg + c];
+            const float y = d.Yp[(size_t)m * d.ldy + c];
+            float g, xh;
+            if (d.bwd_res == URED_ACT_RES) {
+                g = dh;
+                xh = (fmaxf(y, 0.f) - mu) * is;
+            } else if (d.bwd_res == URED_ACT_BN) {
+                g = dh;
+                xh = (y - mu) * is;
+            } else {
+                g = (__builtin_fmaf(y, sc, sh) > 0.f) ? dh : 0.f;
+                xh = (y - mu) * is;
+            }
+            d.C[(size_t)m * d.ldc + c] = g;
+            a1 += g;
+            a2 += g * xh;
+        }
+    }
+    red[0][t] = a1;
+    red[1][t] = a2;
+    __syncthreads();
+    if (t < N) {
+        float s1 = 0.f, s2 = 0.f;
+        for (int q = 0; q < rg; ++q) { s1 += red[0][q * N + t]; s2 += red[1][q * N + t]; }
+        d.bwd_ws[(size_t)blockIdx.x * 2 * N + t] = s1;
+        d.bwd_ws[(size_t)blockIdx.x * 2 * N + N + t] = s2;
+    }
+}
+
+
+// ---- edge-layer forward with BN statistics (K <= 4: the xyz input layers) ----------------
+// Y[m][c] = sum_k X[m][k] W[c][k] + bias[c], stored, and the EPI_FWD per-128-row-block
+// partials {block mean, M2 about it} of p = (stat_relu ? relu(Y) : Y) in stat_ws, two passes
+// like epilogue() (the second recomputes Y from the 12-byte rows instead of re-reading it).
+template <int KS>
+__global__ __launch_bounds__(SMALL_NT) void fwd_small_stats_kernel(const UredGemmDesc d) {
+    __shared__ float red[SMALL_NT];
+    __shared__ float cmean[256];
+    const int N = d.N, rg = SMALL_NT / N, t = threadIdx.x;
+    const int c = t % N, g0 = t / N;
+    const int m0 = blockIdx.x * BM;
+    const int mend = min(m0 + BM, d.M);
+    const bool act = g0 < rg;
+    float w[KS];
+    float bs = 0.f;
+    if (act) {
+#pragma unroll
+        for (int k = 0; k < KS; ++k) w[k] = d.B[(size_t)c * d.ldb + k];
+        if (d.bias) bs = d.bias[c];
+    }
+    auto yv = [&](int m) {
+        const float* a = d.A + (size_t)m * d.lda;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) acc = __builtin_fmaf(a[k], w[k], acc);
+        return acc + bs;
+    };
+    float s1 = 0.f;
+    if (act) {
+#pragma unroll 4
+        for (int m = m0 + g0; m < mend; m += rg) {
+            const float v = yv(m);
+            d.C[(size_t)m * d.ldc + c] = v;
+            s1 += d.stat_relu ? fmaxf(v, 0.f) : v;
+        }
+    }
+    red[t] = s1;
+    __syncthreads();
+    if (t < N) {
+        float sum = 0.f;
+        for (int q = 0; q < rg; ++q) sum += red[q * N + t];
+        cmean[t] = sum / (float)(mend - m0);
+    }
+    __syncthreads();
+    float s2 = 0.f;
+    if (act) {
+        const float mu = cmean[c];
+#pragma unroll 4
+        for (int m = m0 + g0; m < mend; m += rg) {
+            const float v = yv(m);
+            const float e = (d.stat_relu ? fmaxf(v, 0.f) : v) - mu;
+            s2 += e * e;
+        }
+    }
+    red[t] = s2;
+    __syncthreads();
+    if (t < N) {
+        float sum = 0.f;
+        for (int q = 0; q < rg; ++q) sum += red[q * N + t];
+        d.stat_ws[(size_t)blockIdx.x * 2 * N + t] = cmean[t];
+        d.stat_ws[(size_t)blockIdx.x * 2 * N + N + t] = sum;
+    }
+}
+
+bool fwd_small_ok(const UredGemmDesc& d) {
+    return URED_DGRAD_SMALL && d.epi == URED_EPI_FWD && !d.a_kmajor && !d.b_kmajor && d.pro_a == URED_PRO_NONE &&
+           d.K >= 1 && d.K <= 4 && d.N >= 1 && d.N <= 256 && !d.pool_ws && !d.rowbias && d.k1 == d.K;
+}
+
+void launch_fwd_small(const UredGemmDesc& d, hipStream_t st) {
+    const dim3 grid((d.M + BM - 1) / BM);
+    switch (d.K) {
+        case 1: hipLaunchKernelGGL(fwd_small_stats_kernel<1>, grid, dim3(SMALL_NT), 0, st, d); break;
+        case 2: hipLaunchKernelGGL(fwd_small_stats_kernel<2>, grid, dim3(SMALL_NT), 0, st, d); break;
+        case 3: hipLaunchKernelGGL(fwd_small_stats_kernel<3>, grid, dim3(SMALL_NT), 0, st, d); break;
+        default: hipLaunchKernelGGL(fwd_small_stats_kernel<4>, grid, dim3(SMALL_NT), 0, st, d); break;
+    }
+}
+
+bool dgrad_small_ok(const UredGemmDesc& d) {
+    return URED_DGRAD_SMALL && d.epi == URED_EPI_BNBWD && !d.a_kmajor && d.b_kmajor && d.K >= 1 && d.K <= 4 &&
+           d.N >= 1 && d.N <= 256 && !d.pool_idx && d.k1 == d.K;
+}
+
+void launch_dgrad_small(const UredGemmDesc& d, hipStream_t st) {
+    const dim3 grid((d.M + BM - 1) / BM);
+    switch (d.K) {
+        case 1: hipLaunchKernelGGL(dgrad_small_bnbwd_kernel<1>, grid, dim3(SMALL_NT), 0, st, d); break;
+        case 2: hipLaunchKernelGGL(dgrad_small_bnbwd_kernel<2>, grid, dim3(SMALL_NT), 0, st, d); break;
+        case 3: hipLaunchKernelGGL(dgrad_small_bnbwd_kernel<3>, grid, dim3(SMALL_NT), 0, st, d); break;
+        default: hipLaunchKernelGGL(dgrad_small_bnbwd_kernel<4>, grid, dim3(SMALL_NT), 0, st, d); break;
+    }
+}
+
 template <bool A_KM, bool B_KM, int PA, int PB, int EPI>
 void launch(const UredGemmDesc& d, hipStream_t st) {
+    if (EPI == URED_EPI_BNBWD && dgrad_small_ok(d)) { launch_dgrad_small(d, st); return; }
+    if (EPI == URED_EPI_FWD && fwd_small_ok(d)) { launch_fwd_small(d, st); return; }
     const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
     dim3 grid(ntm * ntn, 1, EPI == URED_EPI_SPLITK ? d.splits : 1);
     if (vec_ok(d) && v2_ok(d) && buf_ok(d)) {
