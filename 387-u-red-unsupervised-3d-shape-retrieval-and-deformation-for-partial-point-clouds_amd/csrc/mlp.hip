@@ -201,6 +201,10 @@ __device__ __forceinline__ void store_kmajor(const RowTile& r, float* S) {
 
 template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; };
 
+// streaming kernels for the K <= 4 edge layers (A/B switches, one per direction)
+#ifndef URED_FWD_SMALL
+#define URED_FWD_SMALL 1
+#endif
 #ifndef URED_DGRAD_SMALL
 #define URED_DGRAD_SMALL 1
 #endif
@@ -1587,8 +1591,10 @@ __global__ __launch_bounds__(SMALL_NT) void fwd_small_stats_kernel(const UredGem
 }
 
 bool fwd_small_ok(const UredGemmDesc& d) {
-    return URED_DGRAD_SMALL && d.epi == URED_EPI_FWD && !d.a_kmajor && !d.b_kmajor && d.pro_a == URED_PRO_NONE &&
-           d.K >= 1 && d.K <= 4 && d.N >= 1 && d.N <= 256 && !d.pool_ws && !d.rowbias && d.k1 == d.K;
+    // the kernel reads A and B raw: no prologue on either operand
+    return URED_FWD_SMALL && d.epi == URED_EPI_FWD && !d.a_kmajor && !d.b_kmajor && d.pro_a == URED_PRO_NONE &&
+           d.pro_b == URED_PRO_NONE && d.K >= 1 && d.K <= 4 && d.N >= 1 && d.N <= 256 && !d.pool_ws && !d.rowbias &&
+           d.k1 == d.K;
 }
 
 void launch_fwd_small(const UredGemmDesc& d, hipStream_t st) {
@@ -1602,8 +1608,9 @@ void launch_fwd_small(const UredGemmDesc& d, hipStream_t st) {
 }
 
 bool dgrad_small_ok(const UredGemmDesc& d) {
-    return URED_DGRAD_SMALL && d.epi == URED_EPI_BNBWD && !d.a_kmajor && d.b_kmajor && d.K >= 1 && d.K <= 4 &&
-           d.N >= 1 && d.N <= 256 && !d.pool_idx && d.k1 == d.K;
+    // the kernel reads A and B raw: no prologue on either operand
+    return URED_DGRAD_SMALL && d.epi == URED_EPI_BNBWD && !d.a_kmajor && d.b_kmajor && d.pro_a == URED_PRO_NONE &&
+           d.pro_b == URED_PRO_NONE && d.K >= 1 && d.K <= 4 && d.N >= 1 && d.N <= 256 && !d.pool_idx && d.k1 == d.K;
 }
 
 void launch_dgrad_small(const UredGemmDesc& d, hipStream_t st) {

@@ -1,18 +1,33 @@
 """Data-parallel U-RED training: one process per GPU, gradients all-reduced over RCCL.
 
-The reference has no distributed path (single GPU, README.md:25); the only
-collective it would issue is the contrastive loss's all_gather
-(loss/contrast_loss.py:35-58), which loss/contrast_loss.py keeps. This adds the
-standard DP step: each rank runs the full step on its own shard of samples
-(weak scaling, bs per GPU fixed), then the gradients of every trained parameter
-that received one (stn1/stn2/part_encoding never do — they are skipped, the
-find_unused_parameters equivalent) are averaged with bucketed all_reduce.
-Buckets are flat fp32 buffers of ~bucket_mb MB, all issued asynchronously (on a
-communication stream for GPU tensors) once backward has finished; at ~69 MB per
-step over xGMI this is a small share of a step (overlap with backward via
-gradient hooks is the next step).
-BatchNorm uses per-rank batch statistics (what DDP does without SyncBN).
+The reference has no distributed path (single GPU, README.md:25); the only collective it would
+issue is the contrastive loss's all_gather (loss/contrast_loss.py:35-58), which
+loss/contrast_loss.py keeps. This adds the standard DP step: each rank runs the full step on its
+own shard of samples (weak scaling, bs per GPU fixed), and the gradients of every parameter
+that has one this step are averaged (stn1/stn2/part_encoding never get one and are skipped: the
+find_unused_parameters equivalent; re_residual_net_full joins once the residual loss switches
+on). BatchNorm uses per-rank batch statistics (what DDP does without SyncBN).
+
+With FlatAdam (the default optimizer on the GPU) the gradients are reduced in place in its flat
+gradient buffer, in buckets of ~bucket_mb MB that are issued DURING backward:
+  * the first step learns the order in which backward produces the gradients (post-accumulate
+    hooks) and FlatAdam lays its flat buffers out in that order, so a bucket is one contiguous
+    range that fills early; the (offset, size, active) layout is checked equal on every rank
+    once (an all-reduce of its hash), so that every rank reduces the same ranges;
+  * from the second step on, each parameter's post-accumulate hook counts its bucket down;
+    a full bucket's gradients are copied into their flat views (one multi-tensor copy) and its
+    all_reduce is issued asynchronously (RCCL runs it on its own stream after the copy, while
+    backward continues on the compute stream). Buckets are issued strictly in index order, as
+    DDP does, so every rank issues the same collectives in the same order;
+  * after backward: buckets that did not fill (a parameter without a gradient this step) are
+    completed with zeros for the missing parameters and reduced; parameters with a gradient
+    outside every bucket (one that just became active) are reduced as extra ranges; then the
+    buckets are rebuilt for the new set. The flat gradient is scaled by 1/world.
+Without FlatAdam (torch's Adam), `make_buckets` / `allreduce_gradients` reduce per bucket after
+backward, rebuilding the buckets whenever the set of parameters with a gradient changes.
 """
+import hashlib
+
 import torch
 import torch.distributed as dist
 
@@ -39,19 +54,12 @@ def allreduce_gradients(buckets, world, stream=None):
     """Average p.grad over the process group, one flat all_reduce per bucket."""
     if world == 1:
         return
-    main = torch.cuda.current_stream() if stream is not None else None
-    if stream is not None:
-        stream.wait_stream(main)
     works = []
-    ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
-    with ctx:
-        for b in buckets:
-            flat = torch.cat([p.grad.reshape(-1) for p in b])
-            works.append((b, flat, dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True)))
+    for b in buckets:
+        flat = torch.cat([p.grad.reshape(-1) for p in b])
+        works.append((b, flat, dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True)))
     for _, _, w in works:
         w.wait()
-    if stream is not None:
-        main.wait_stream(stream)
     inv = 1.0 / world
     for b, flat, _ in works:
         flat.mul_(inv)
@@ -60,37 +68,161 @@ def allreduce_gradients(buckets, world, stream=None):
             n = p.numel()
             p.grad.copy_(flat[off:off + n].view_as(p.grad))
             off += n
-        if stream is not None:
-            flat.record_stream(main)
 
 
-def allreduce_flat(flat, world, bucket_elems, stream=None):
-    """Average a flat gradient buffer over the process group: all_reduce on ~bucket_elems views
-    of it in place (no gather/scatter copies), all issued before the first wait."""
-    main = torch.cuda.current_stream() if stream is not None else None
-    if stream is not None:
-        stream.wait_stream(main)
-    ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
-    with ctx:
-        works = [dist.all_reduce(flat[o:o + bucket_elems], op=dist.ReduceOp.SUM, async_op=True)
-                 for o in range(0, flat.numel(), bucket_elems)]
+def allreduce_flat(flat, world, bucket_elems, ranges=None):
+    """Average the given [beg, end) ranges of a flat gradient buffer over the process group:
+    all_reduce on <= bucket_elems views in place, all issued before the first wait."""
+    ranges = ranges or [(0, flat.numel())]
+    works = []
+    for b, e in ranges:
+        for o in range(b, e, bucket_elems):
+            works.append(dist.all_reduce(flat[o:min(e, o + bucket_elems)], op=dist.ReduceOp.SUM, async_op=True))
     for w in works:
         w.wait()
-    if stream is not None:
-        main.wait_stream(stream)
-    flat.mul_(1.0 / world)
+    for b, e in ranges:
+        flat[b:e].mul_(1.0 / world)
 
 
-class _nullctx:
-    def __enter__(self):
-        return self
+def layout_hash(key):
+    """A 62-bit hash of a FlatAdam layout key (identical on every rank of a correct job)."""
+    return int.from_bytes(hashlib.sha256(repr(key).encode()).digest()[:8], "little") >> 2
 
-    def __exit__(self, *a):
-        return False
+
+class _Bucket:
+    __slots__ = ("idx", "beg", "end", "params", "views", "pending", "launched", "work")
+
+    def __init__(self, idx, beg, end, params, views):
+        self.idx, self.beg, self.end, self.params, self.views = idx, beg, end, params, views
+        self.pending, self.launched, self.work = len(params), False, None
+
+
+class FlatGradReducer:
+    """Bucketed all-reduce of FlatAdam's flat gradient, issued from backward's gradient hooks
+    (see the module docstring). Usage per step: begin() before backward, finish() after it."""
+
+    def __init__(self, optimizer, params, world, bucket_elems, overlap=True):
+        self.opt, self.world, self.bucket_elems, self.overlap = optimizer, world, bucket_elems, overlap
+        self._arrival = []                  # first step: gradient arrival order
+        self._fb = None                     # buckets over the flat gradient
+        self._fb_key = None
+        self._bucket_of = {}
+        self._next = 0
+        self._armed = False
+        self._step_armed = False
+        self._checked = False
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params] if overlap else []
+
+    # hooks run on the autograd thread, in gradient-production order
+    def _on_grad(self, p):
+        if not self._armed:
+            if self._fb is None:
+                self._arrival.append(p)
+            return
+        b = self._bucket_of.get(id(p))
+        if b is None:
+            return                        # not in a bucket: handled after backward
+        b.pending -= 1
+        if b.pending == 0 and b.idx == self._next:
+            fb = self._fb
+            while self._next < len(fb) and fb[self._next].pending == 0:
+                self._launch(fb[self._next])
+                self._next += 1
+
+    def _launch(self, b, fill_missing=False):
+        dst, src = [], []
+        for p, v in zip(b.params, b.views):
+            g = p.grad
+            if g is None:
+                if fill_missing:
+                    v.zero_()
+                continue
+            if g.data_ptr() != v.data_ptr():
+                dst.append(v)
+                src.append(g)
+        if dst:
+            torch._foreach_copy_(dst, src)
+        b.work = dist.all_reduce(self.opt.flat_grad[b.beg:b.end], op=dist.ReduceOp.SUM, async_op=True)
+        b.launched = True
+
+    def _build(self):
+        from ured_hip.optim import _aligned
+        opt = self.opt
+        slot = sorted((opt._off[i], i) for i, a in enumerate(opt._active) if a)
+        fb, cur, beg, end, n = [], [], 0, 0, 0
+        for o, i in slot:
+            if cur and (o != end or n >= self.bucket_elems):
+                fb.append(_Bucket(len(fb), beg, end, [opt.params_all[j] for j in cur], [opt._gviews[j] for j in cur]))
+                cur, n = [], 0
+            if not cur:
+                beg = o
+            cur.append(i)
+            end = o + _aligned(opt.params_all[i].numel())
+            n += opt.params_all[i].numel()
+        if cur:
+            fb.append(_Bucket(len(fb), beg, end, [opt.params_all[j] for j in cur], [opt._gviews[j] for j in cur]))
+        self._fb, self._fb_key = fb, opt._active
+        self._bucket_of = {id(p): b for b in fb for p in b.params}
+
+    def _check_layout(self):
+        h = layout_hash(self.opt.layout_key())
+        t = torch.tensor([h, -h], dtype=torch.int64, device=self.opt.flat_grad.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if int(t[0]) != h or -int(t[1]) != h:
+            raise RuntimeError("data-parallel: the flat gradient layout differs between ranks "
+                               "(different parameter sets with gradients); refusing to all-reduce")
+        self._checked = True
+
+    @property
+    def num_buckets(self):
+        return 0 if self._fb is None else len(self._fb)
+
+    def begin(self):
+        """Before backward: arm the hooks (from the second step on)."""
+        self._step_armed = self._fb is not None
+        if self._step_armed:
+            for b in self._fb:
+                b.pending, b.launched, b.work = len(b.params), False, None
+            self._next = 0
+        self._armed = self._step_armed
+
+    def finish(self):
+        """After backward: complete the reduction; the flat gradient holds the rank average and
+        p.grad of every active parameter is its flat view."""
+        self._armed = False
+        armed, self._step_armed = self._step_armed, False
+        opt = self.opt
+        if opt.flat_param is None and self._arrival:
+            opt.layout_order = list(self._arrival)        # first step: backward's order
+        active = opt.prepare()
+        if not self._checked:
+            self._check_layout()
+        if not armed or not any(b.launched for b in self._fb):
+            # first step (overlap off, a captured step, or no bucket filled): all after backward
+            opt.gather_grads()
+            allreduce_flat(opt.flat_grad, self.world, self.bucket_elems, opt.active_ranges())
+            if self.overlap and self._fb_key != active:
+                self._build()
+            return
+        for b in self._fb[self._next:]:                   # buckets that did not fill, in order
+            self._launch(b, fill_missing=True)
+        extra = [i for i, a in enumerate(active) if a and id(opt.params_all[i]) not in self._bucket_of]
+        for i in extra:                                   # parameters that just became active
+            opt._gviews[i].copy_(opt.params_all[i].grad)
+        for b in self._fb:
+            b.work.wait()
+        if extra:
+            allreduce_flat(opt.flat_grad, self.world, self.bucket_elems,
+                           [(opt._off[i], opt._off[i] + opt.params_all[i].numel()) for i in extra])
+        for b in self._fb:
+            opt.flat_grad[b.beg:b.end].mul_(1.0 / self.world)
+        opt.mark_gathered()
+        if self._fb_key != active:
+            self._build()
 
 
 class DataParallelStep(TrainStep):
-    def __init__(self, cfg, db, device, bucket_mb=25.0):
+    def __init__(self, cfg, db, device, bucket_mb=25.0, overlap=None):
         super().__init__(cfg, db, device)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         params = []
@@ -98,18 +230,29 @@ class DataParallelStep(TrainStep):
             params += [p for p in self.models[name].parameters() if p.requires_grad]
         self.params = params[::-1]          # ~ the order backward produces gradients
         self.bucket_elems = int(bucket_mb * 1e6 / 4)
-        self._buckets = None
-        on_gpu = torch.device(device).type == "cuda"
-        self.comm_stream = torch.cuda.Stream(device=device) if (self.world > 1 and on_gpu) else None
+        self._buckets = None                # torch-Adam path: (active key, buckets)
+        overlap = (self.world > 1) if overlap is None else bool(overlap)
+        self.reducer = (FlatGradReducer(self.optimizer, params, self.world, self.bucket_elems, overlap)
+                        if self.world > 1 and hasattr(self.optimizer, "prepare") else None)
+
+    def step(self, batch, epoch=0):
+        self.optimizer.zero_grad(set_to_none=True)
+        loss, T = self.forward(batch, epoch)
+        if self.reducer is not None:
+            self.reducer.begin()
+        loss.backward()
+        self.reduce_gradients()
+        self.clip_and_step()
+        return T
 
     def reduce_gradients(self):
         if self.world == 1:
             return
-        if getattr(self.optimizer, "flat_param", None) is not None:
-            # FlatAdam: gather the gradients into its flat buffer once, all-reduce that in place
-            self.optimizer.gather_grads()
-            allreduce_flat(self.optimizer.flat_grad, self.world, self.bucket_elems, self.comm_stream)
+        if self.reducer is not None:
+            self.reducer.finish()
             return
-        if self._buckets is None:           # first step: learn which parameters receive gradients
-            self._buckets = make_buckets(self.params, self.bucket_elems)
-        allreduce_gradients(self._buckets, self.world, self.comm_stream)
+        # torch's Adam: per-bucket reduction after backward; buckets follow the active set
+        key = tuple(p.grad is not None for p in self.params)
+        if self._buckets is None or self._buckets[0] != key:
+            self._buckets = (key, make_buckets(self.params, self.bucket_elems))
+        allreduce_gradients(self._buckets[1], self.world)

@@ -10,12 +10,15 @@ are built on the device or from host labels before the step), so it is captured 
   eager                : reduce_gradients()      (RCCL bucketed all-reduce when world > 1)
   graph "update"       : clip_grad_norm_ x6 + Adam (capturable)
 
-key = the batch's padded distinct-source-part count (UniqueRows with a bucket; None when the
-batch encodes every slot): one forward/backward graph per key, captured the first time the key
+key = (the batch's padded distinct-source-part count (UniqueRows with a bucket; None when the
+batch encodes every slot), the residual-loss gate `epoch > init_p_m_loss`): one forward/backward
+graph per key, captured the first time the key
 is seen, right after that batch's step runs eagerly (so no extra optimizer step is taken and
 the capture finds libraries and workspaces initialised). At most `max_graphs` are kept (LRU).
 Gradients live in persistent tensors that every graph zeroes and accumulates into, so the one
-update graph serves all of them.
+update graph serves all of them. When the gate flips, the set of parameters with a gradient
+changes (re_residual_net_full joins): every graph, the update graph and the persistent
+gradients are dropped and the next step runs eagerly again.
 
 Same kernels, same arithmetic as the eager step: a replay is bit-identical to an eager step on
 the same state and batch. With world > 1 the forward contains the contrastive loss's
@@ -61,10 +64,13 @@ class GraphedStep:
     def optimizer(self):
         return self.inner.optimizer
 
-    @staticmethod
-    def key(batch):
+    def gate(self, epoch):
+        cfg = self.inner.cfg
+        return bool(cfg["use_residuals_reg"] > 0.0 and epoch > cfg["init_p_m_loss"])
+
+    def key(self, batch, epoch=0):
         uq = batch.get("src_unique")
-        return None if uq is None else uq.U
+        return (None if uq is None else uq.U, self.gate(epoch))
 
     def _eager(self, batch, epoch):
         if self.grads is None:                       # first step: torch allocates the grads
@@ -100,7 +106,12 @@ class GraphedStep:
             self.graphs.popitem(last=False)
 
     def step(self, batch, epoch=0):
-        k = self.key(batch)
+        k = self.key(batch, epoch)
+        if self.grads is not None and getattr(self, "_gate", None) is not None and k[1] != self._gate:
+            self.graphs.clear()          # another parameter set: re-learn the gradients eagerly
+            self.g_update = None
+            self.grads = None
+        self._gate = k[1]
         ent = self.graphs.get(k)
         if ent is None:
             # the batch's real step runs eagerly on a side stream (that also warms up library

@@ -12,7 +12,10 @@ working path is engine/vis.py:118-256, restated here batched and without host sy
   6. (optional) the residual-net score max_points sum|r| (vis.py:221-231), NDCG@40 of the
      retrieval scores against the pseudo-label rows (cal_retrieval_score, vis.py:207), and the
      retrieved meshes deformed with the target parts' boxes as default (vis.py:278-296)
-    python engine/test.py [config.json]
+    python engine/test.py [config.json]       (default config/config_vis_test.json, the reference's
+                                              inference schema read by engine/vis.py:29; its
+                                              init_dm / init_re checkpoints are loaded as the
+                                              reference does, get_models)
 """
 import json
 import os
@@ -134,8 +137,13 @@ class GraphedInfer:
 
 
 def main(cfg):
+    for key in ("dm_model_path", "re_model_path"):
+        flag = "init_dm" if key == "dm_model_path" else "init_re"
+        if cfg.get(flag) and not os.path.exists(cfg[key]):
+            raise FileNotFoundError(f"{flag} is set but {cfg[key]} does not exist (train first: "
+                                    f"python engine/train.py writes {cfg.get('log_path', '.')}/checkpoint_*.pth)")
     device = cfg["device"]
-    db, _ = load_sources(cfg, device)
+    db, _ = load_sources(dict(cfg, compute_connectivity=False), device)
     models, _, _ = get_models(cfg, device)
     codes = encode_sources(models, db)
     for i in range(int(cfg.get("iters_per_epoch", 2))):
@@ -146,5 +154,5 @@ def main(cfg):
 
 
 if __name__ == "__main__":
-    path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(_HERE), "config", "config_train_test.json")
+    path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(_HERE), "config", "config_vis_test.json")
     main(json.load(open(path)))

@@ -3,6 +3,10 @@
   python engine/train.py [config.json]          (the reference ignores argv and
                                                   hard-codes config/config_train_test.json,
                                                   engine/train.py:362-364; argv is honoured here)
+  torchrun --nproc-per-node N engine/train.py [config.json]
+                                                 data-parallel: one process per GPU, bs per GPU,
+                                                 gradients all-reduced over RCCL during backward
+                                                 (engine/dp.py); rank 0 logs and saves
 
 One iteration (engine/train.py:196-345) = source/target encoders, part pooling,
 three residual nets, DeformNet, get_shape, the chamfer / contrast / symmetry /
@@ -14,8 +18,11 @@ Adam. Differences that do not change results:
   * the embedding layer's gradient is not computed: the reference excludes it from
     the optimizer (train_utils/optimizer_dm.py:83) and never reads it;
   * per-step scalar logging (which forces .item() host syncs) is optional (cfg["log_every"]).
-Data: cfg["synthetic"] (default) generates SURVEY §8(d) batches; the reference's
-on-disk PartNet/pickle pipeline is out of scope this round.
+Data: cfg["synthetic"] (default) generates SURVEY §8(d) targets; the source labels come from
+the reference's pseudo-label selection (get_labels, dataset/dataset_utils.py:1101-1143) over a
+target-part x source calc_dcd table computed once on the GPU and the sources_connect matrix
+(PseudoLabelLoader; cfg["pseudo_labels"]: false draws them uniformly instead). The reference's
+on-disk PartNet h5 readers are out of scope (h5py is not in this image).
 """
 import datetime
 import json
@@ -316,6 +323,79 @@ def batch_to_device(b, device, num_sources=None, bucket=None):
     return out
 
 
+def make_loader(cfg, db, device, seed=0, dist_src=None):
+    if cfg.get("pseudo_labels", True) and dist_src is not None and torch.device(device).type == "cuda":
+        return PseudoLabelLoader(cfg, db, device, dist_src, seed=seed)
+    return SyntheticLoader(cfg, db.num_sources, device, seed=seed)
+
+
+def resample_parts(x, labels, k, n=1024, seed=0):
+    """[k, n, 3] part clouds of one target (each part's points drawn with replacement and
+    normalised, like the reference's 1024-point part h5 clouds, generate_pair.py:87-122)."""
+    from engine.generate_pair import normalize_pts
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = np.zeros((k, n, 3), np.float32)
+    for i in range(k):
+        pts = x[labels == i]
+        out[i] = normalize_pts(pts[rng.integers(0, pts.shape[0], size=n)])
+    return out
+
+
+class PseudoLabelLoader:
+    """DataLoader(partnet_dataset) + get_labels (engine/train.py:167-197,
+    dataset/dataset_utils.py:1101-1143) on a fixed synthetic target set: cfg["num_targets"]
+    targets (SURVEY §8(d) generator), their part clouds scored against every source by calc_dcd
+    once on the GPU (PairGenerator.cross: the per-part pickle rows of generate_pair.py), and
+    the labels chosen by the reference's rule on the device (PseudoLabelTable: top-10 by cd_m,
+    < filter_threshold, semantic preference, mask_label over dist_src's cd_m with cl_k). The
+    table is deterministic, so the labels of every target are computed once and kept on the
+    host (the unique-source tables of a batch are then built without a device sync). Epochs
+    visit the targets in a seeded shuffle (drop_last, as the reference's DataLoader)."""
+
+    def __init__(self, cfg, db, device, dist_src, seed=0):
+        from engine.generate_pair import PairGenerator, normalize_pts
+        from train_utils.pseudo_labels import PseudoLabelTable
+        self.cfg, self.db, self.device, self.seed = cfg, db, device, seed
+        P = cfg["MAX_NUM_PARTS"]
+        T = int(cfg.get("num_targets", 128))
+        self.bs = cfg["batch_size"]
+        t = synthetic.make_batch(T, cfg.get("num_points", 2048), db.num_sources, max_parts=P,
+                                 parts=cfg.get("parts", 4), seed=seed * 7777 + 17)
+        self.targets = t
+        rows = np.full((T, P), -1, np.int64)
+        clouds, part_sem = [], []
+        for j in range(T):
+            k = int(t["parts"][j])
+            clouds.append(resample_parts(t["x"][j], t["labels"][j], k, db.points.shape[1], seed=seed * 131 + j))
+            for i in range(k):
+                rows[j, i] = len(part_sem)
+                part_sem.append(int(t["tgt_sem"][j][t["labels"][j] == i][0]))
+        src = np.stack([normalize_pts(p) for p in db.points.cpu().numpy()])
+        gen = PairGenerator(torch.from_numpy(src).to(device))
+        table = gen.cross(torch.from_numpy(np.concatenate(clouds)))          # [3, parts, NS]
+        self.table = PseudoLabelTable(table[2], part_sem, db.sem, np.asarray(dist_src)[2],
+                                      alpha=cfg.get("filter_threshold", 2e-2), cl_k=cfg.get("cl_k", 40),
+                                      device=device)
+        self.part_rows = rows
+        self.labels = self.table.labels(torch.from_numpy(rows).to(device)).cpu().numpy()
+        self.n = T // self.bs
+        self.epoch = 0
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        rng = np.random.Generator(np.random.PCG64([self.seed, self.epoch]))
+        self.epoch += 1
+        order = rng.permutation(self.targets["x"].shape[0])
+        for i in range(self.n):
+            sel = order[i * self.bs:(i + 1) * self.bs]
+            b = {"x": self.targets["x"][sel], "labels": self.targets["labels"][sel],
+                 "tgt_sem": self.targets["tgt_sem"][sel], "src_labels": self.labels[sel]}
+            yield batch_to_device(b, self.device, self.db.num_sources,
+                                  bucket=8 if self.cfg.get("cuda_graph") else None)
+
+
 class SyntheticLoader:
     """Stands in for DataLoader(partnet_dataset) + get_labels (engine/train.py:167-197)."""
 
@@ -364,25 +444,52 @@ def save_model(model, start, epoch, cfg):
     print(log)
 
 
+def init_distributed(cfg):
+    """torchrun environment -> (rank, world, device). One process per GPU; RCCL ("nccl") on
+    ROCm devices, gloo on CPU. Single process: (0, 1, cfg["device"])."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return 0, 1, cfg["device"]
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if str(cfg["device"]).startswith("cuda"):
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+        dist.init_process_group("nccl", device_id=device)
+    else:
+        device = torch.device(cfg["device"])
+        dist.init_process_group("gloo")
+    return dist.get_rank(), dist.get_world_size(), device
+
+
 def main(cfg):
-    device = cfg["device"]
-    db, _ = load_sources(cfg, device)
-    trainer = TrainStep(cfg, db, device)
-    loader = SyntheticLoader(cfg, db.num_sources, device, seed=int(cfg.get("seed", 0)))
-    writer = _ScalarLog(cfg["log_path"])
+    rank, world, device = init_distributed(cfg)
+    db, dist_src = load_sources(cfg, device)
+    if world > 1:
+        from engine.dp import DataParallelStep
+        trainer = DataParallelStep(cfg, db, device)
+    else:
+        trainer = TrainStep(cfg, db, device)
+    # each rank draws its own shard of samples (weak scaling: batch_size per GPU)
+    loader = make_loader(cfg, db, device, seed=int(cfg.get("seed", 0)) + 7919 * rank, dist_src=dist_src)
+    writer = _ScalarLog(cfg["log_path"]) if rank == 0 else None
     log_every = int(cfg.get("log_every", 1))
     for epoch in range(cfg["epochs"]):
         start = datetime.datetime.now()
-        print(str(start), "training epoch", str(epoch))
+        if rank == 0:
+            print(str(start), "training epoch", str(epoch))
         for i, batch in enumerate(loader):
             T = trainer.step(batch, epoch)
-            if log_every and i % log_every == 0:
+            if writer is not None and log_every and i % log_every == 0:
                 for tag, v in T.items():
                     if not tag.startswith("_") and tag != "ref_cd_loss_part":
                         writer.add_scalar(tag, float(v.item()), epoch * len(loader) + i)
         trainer.scheduler.step()
-        if (epoch + 1) % cfg["save_epoch"] == 0:
+        if rank == 0 and (epoch + 1) % cfg["save_epoch"] == 0:
             save_model(trainer.state_dict(), start, epoch, cfg)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
     return trainer
 
 

@@ -2,10 +2,16 @@
 
 The reference loads one h5 per source part (points[1024,3], points_mat[3072,6],
 default_param[6], semantic label, mesh) into a list of dicts plus the
-sources_connect.npy distance matrix. Here the arrays live in HBM as stacked
-tensors (SourceDB) so the per-step gathers are device ops. With cfg["synthetic"]
-the arrays come from dataset.synthetic.make_source_db.
+sources_connect.npy distance matrix (`dist_src`, load_sources.py:13: [3, NS, NS] = dcd, cd_s,
+cd_m of every source pair, engine/visualization.py:30-46). Here the arrays live in HBM as
+stacked tensors (SourceDB) so the per-step gathers are device ops. With cfg["synthetic"]
+the arrays come from dataset.synthetic.make_source_db. `dist_src` is read from
+cfg["src_connectivity"] when that .npy exists (np.load without pickles); otherwise it is
+computed on the device from the source clouds by the same all-pairs calc_dcd as the
+reference's offline generator (engine/generate_pair.py PairGenerator + connect_matrix).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -32,5 +38,22 @@ def load_sources(cfg, device=None):
     n = 512 if n <= 0 else n
     d = synthetic.make_source_db(n, seed=int(cfg.get("seed", 0)) + 1)
     db = SourceDB(d["src_points"], d["src_mats"], d["src_default_param"], d["src_sem"], device)
-    dist_src = np.zeros((3, n, n), np.float32)
+    path = cfg.get("src_connectivity")
+    if path and os.path.exists(path):
+        dist_src = np.load(path, allow_pickle=False)
+        if dist_src.shape != (3, n, n):
+            raise ValueError(f"{path}: expected [3, {n}, {n}], got {dist_src.shape}")
+    elif cfg.get("compute_connectivity", True) and torch.device(device).type == "cuda":
+        dist_src = source_connectivity(db)
+    else:
+        dist_src = np.zeros((3, n, n), np.float64)
     return db, dist_src
+
+
+def source_connectivity(db):
+    """[3, NS, NS] (dcd, cd_s, cd_m) of every pair of normalised source clouds: the reference's
+    sources_connect.npy (generate_pair.get_src_pair rows + visualization.py:30-46)."""
+    from engine.generate_pair import PairGenerator, connect_matrix, normalize_pts
+    pts = np.stack([normalize_pts(p) for p in db.points.cpu().numpy()])
+    gen = PairGenerator(torch.from_numpy(pts).to(db.points.device))
+    return connect_matrix(gen.rows(range(db.num_sources)), db.num_sources)

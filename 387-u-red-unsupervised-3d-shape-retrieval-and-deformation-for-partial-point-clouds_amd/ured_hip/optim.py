@@ -3,26 +3,34 @@ flat HBM buffers (ured_adam_clip_step, csrc/optim.hip).
 
 The reference's step tail (engine/train.py:331-346) is six clip_grad_norm_(module, 5.0) calls
 and torch.optim.Adam (train_utils/optimizer_dm.py:68-104). torch's fused Adam plus the clip
-walk ~500 tensors per step in multi-tensor chunks; here, at the first step (when it is known
-which parameters receive gradients — stn1/stn2/part_encoding never do, and Adam skips them),
-every trained parameter moves into one flat buffer (16-float aligned slices, grouped by
-module; `p.data` becomes a view of it), with flat gradient and moment buffers beside it. Each
-step then gathers the step's gradients into the flat gradient (one multi-tensor copy) and
-runs three launches: per-chunk fp64 sums of squares, per-module clip factors (and the device
-step counter), one float4 stream over p / g / exp_avg / exp_avg_sq.
+walk ~500 tensors per step in multi-tensor chunks; here, at the first step, every parameter of
+the six modules moves into one flat buffer (16-float aligned slices; `p.data` becomes a view of
+it), with flat gradient and moment buffers beside it. Each step then gathers the step's
+gradients into the flat gradient (one multi-tensor copy) and runs three launches: per-chunk fp64
+sums of squares, per-module clip factors (and the per-parameter device step counters), one
+float4 stream over p / g / exp_avg / exp_avg_sq.
+
+Which parameters take a step is decided per step, as torch does: a parameter without a gradient
+(`p.grad is None`: stn1/stn2/part_encoding always, re_residual_net_full until the residual loss
+is switched on at epoch > init_p_m_loss) is left out of the clip norms and of Adam (no weight
+decay, no moment decay, its step count does not advance). Chunks never straddle a parameter;
+only the active parameters' chunks are listed, and the list is rebuilt when the set of
+parameters with a gradient changes. The layout (slice order) is fixed at the first step:
+the parameters active then come first, in `layout_order` if one was given (engine/dp.py passes
+the order in which the first backward produced the gradients, so that its buckets fill early),
+the others after them.
 
 The gradients are gathered rather than accumulated in place: with `p.grad` kept as a view of
 the flat buffer, autograd would add every new gradient into it (one extra add launch per
-parameter, measured −1.2 % per step); with zero_grad(set_to_none=True) autograd hands over
+parameter, measured -1.2 % per step); with zero_grad(set_to_none=True) autograd hands over
 fresh gradient tensors and the gather is one copy.
 
 Semantics kept: after step() (and after gather_grads(), which engine/dp.py calls before its
-all-reduce of the flat gradient) `p.grad` is a view of the flat gradient and holds the clipped
-gradient (clip_grad_norm_ scales in place); the learning rate is read from
-param_groups[0]["lr"] on every step (StepLR works unchanged) and copied to a device scalar
-only when it changes (call sync_lr() before replaying a captured step after an lr change).
-Parameters that never received a gradient at the first step are left untouched, as torch's
-Adam does. optimizer.state holds the flat moments under "flat" (not per parameter).
+all-reduce of the flat gradient) `p.grad` of every active parameter is a view of the flat
+gradient and holds the clipped gradient (clip_grad_norm_ scales in place); the learning rate is
+read from param_groups[0]["lr"] on every step (StepLR works unchanged) and copied to a device
+scalar only when it changes (call sync_lr() before replaying a captured step after an lr
+change). optimizer.state holds the flat moments and the per-parameter step counts under "flat".
 """
 import ctypes
 
@@ -32,11 +40,15 @@ from . import _lib
 from .kernels import _p
 
 _P, _I, _F, _D = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double
-_lib.register({"ured_adam_clip_step": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _F, _P, _P,
+_lib.register({"ured_adam_clip_step": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _F, _P, _P, _P, _I,
                                        _D, _D, _D, _D, _P, _P, _P]})
 
-CHUNK = 8192          # elements per workgroup (never straddles a module segment)
+CHUNK = 8192          # elements per workgroup (never straddles a parameter)
 ALIGN = 16            # each parameter slice starts on a 64-B boundary
+
+
+def _aligned(n):
+    return -(-n // ALIGN) * ALIGN
 
 
 class FlatAdam(torch.optim.Optimizer):
@@ -48,49 +60,97 @@ class FlatAdam(torch.optim.Optimizer):
         self.flat_param = self.flat_grad = None
         self._lr_t, self._lr_host = None, None
         self._gathered = False
+        self._active = None
+        self.layout_order = None        # optional: parameter order for the flat layout (see module doc)
 
     # ---- layout -------------------------------------------------------------------------
-    def _flatten(self):
+    def _flatten(self, active_ids):
         dev = self.param_groups[0]["params"][0].device
-        seg_params, offs, total = [], [], 0
-        for seg in self._segments:
-            ps = [p for p in seg if p.grad is not None]
-            o = []
-            for p in ps:
-                o.append(total)
-                total += -(-p.numel() // ALIGN) * ALIGN
-            seg_params.append(ps)
-            offs.append(o)
+        seen, plist, seg_of = set(), [], []
+        for si, seg in enumerate(self._segments):
+            for p in seg:
+                if id(p) not in seen and p.requires_grad:
+                    seen.add(id(p))
+                    plist.append(p)
+                    seg_of.append(si)
+        rank = {id(p): i for i, p in enumerate(plist)}
+        if self.layout_order is not None:
+            pos = {id(p): i for i, p in enumerate(self.layout_order)}
+            first = sorted((i for i, p in enumerate(plist) if id(p) in active_ids),
+                           key=lambda i: (pos.get(id(plist[i]), len(pos)), i))
+        else:
+            first = [i for i, p in enumerate(plist) if id(p) in active_ids]
+        rest = [i for i in range(len(plist)) if id(plist[i]) not in active_ids]
+        off, total = [0] * len(plist), 0
+        for i in first + rest:
+            off[i] = total
+            total += _aligned(plist[i].numel())
+        self.params_all, self._seg_of, self._off, self._rank = plist, seg_of, off, rank
         self.flat_param = torch.zeros(total, device=dev)
         self.flat_grad = torch.zeros(total, device=dev)
         self.exp_avg = torch.zeros(total, device=dev)
         self.exp_avg_sq = torch.zeros(total, device=dev)
-        cb, ce, cs, s0 = [], [], [], [0]
         self._gviews = []
-        for si, (ps, o) in enumerate(zip(seg_params, offs)):
-            for p, off in zip(ps, o):
-                n = p.numel()
-                self.flat_param[off:off + n].copy_(p.detach().reshape(-1))
-                p.data = self.flat_param[off:off + n].view_as(p)
-                self._gviews.append(self.flat_grad[off:off + n].view_as(p))
-            if ps:
-                beg, end = o[0], o[-1] + -(-ps[-1].numel() // ALIGN) * ALIGN
+        for p, o in zip(plist, off):
+            n = p.numel()
+            self.flat_param[o:o + n].copy_(p.detach().reshape(-1))
+            p.data = self.flat_param[o:o + n].view_as(p)
+            self._gviews.append(self.flat_grad[o:o + n].view_as(p))
+        self._nseg = len(self._segments)
+        self._coef = torch.ones(self._nseg, device=dev)
+        self._lr_t = torch.zeros(1, device=dev)
+        self._pstep = torch.zeros(len(plist), device=dev)
+        self.state["flat"] = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "step": self._pstep}
+        self._active = None
+
+    def _set_active(self, active):
+        """Chunk tables of the parameters flagged in `active` (one bool per params_all entry),
+        segment-major so that each module's chunks are contiguous."""
+        dev = self.flat_param.device
+        cb, ce, cs, cp, s0 = [], [], [], [], [0]
+        for si in range(self._nseg):
+            for i, p in enumerate(self.params_all):
+                if self._seg_of[i] != si or not active[i]:
+                    continue
+                beg = self._off[i]
+                end = beg + _aligned(p.numel())
                 for b in range(beg, end, CHUNK):
                     cb.append(b)
                     ce.append(min(end, b + CHUNK))
                     cs.append(si)
+                    cp.append(i)
             s0.append(len(cb))
-        self.flat_params_list = [p for ps in seg_params for p in ps]
-        self._cbeg = torch.tensor(cb, dtype=torch.int64, device=dev)
-        self._cend = torch.tensor(ce, dtype=torch.int64, device=dev)
-        self._cseg = torch.tensor(cs, dtype=torch.int32, device=dev)
+        act = [i for i, a in enumerate(active) if a]
+        self._cbeg = torch.tensor(cb or [0], dtype=torch.int64, device=dev)
+        self._cend = torch.tensor(ce or [0], dtype=torch.int64, device=dev)
+        self._cseg = torch.tensor(cs or [0], dtype=torch.int32, device=dev)
+        self._cpar = torch.tensor(cp or [0], dtype=torch.int32, device=dev)
         self._seg0 = torch.tensor(s0, dtype=torch.int32, device=dev)
-        self._nchunks, self._nseg = len(cb), len(self._segments)
+        self._act = torch.tensor(act or [0], dtype=torch.int32, device=dev)
+        self._nact = len(act)
+        self._nchunks = len(cb)
         self._partial = torch.zeros(max(len(cb), 1), dtype=torch.float64, device=dev)
-        self._coef = torch.ones(self._nseg, device=dev)
-        self._lr_t = torch.zeros(1, device=dev)
-        self._step_t = torch.zeros(1, device=dev)
-        self.state["flat"] = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "step": self._step_t}
+        self._active = tuple(active)
+
+    def active_ranges(self):
+        """Flat-buffer ranges [beg, end) covering the active parameters (merged where adjacent)."""
+        spans = sorted((self._off[i], self._off[i] + _aligned(p.numel()))
+                       for i, p in enumerate(self.params_all) if self._active[i])
+        out = []
+        for b, e in spans:
+            if out and out[-1][1] == b:
+                out[-1][1] = e
+            else:
+                out.append([b, e])
+        return [tuple(r) for r in out]
+
+    def layout_key(self):
+        """(offset, numel) of every parameter slice and the active flags: equal on every rank
+        of a data-parallel job (engine/dp.py checks it once)."""
+        return tuple((o, p.numel(), bool(a)) for o, p, a in zip(self._off, self.params_all, self._active))
+
+    def current_active(self):
+        return tuple(p.grad is not None for p in self.params_all)
 
     def sync_lr(self):
         lr = float(self.param_groups[0]["lr"])
@@ -98,25 +158,41 @@ class FlatAdam(torch.optim.Optimizer):
             self._lr_t.fill_(lr)
             self._lr_host = lr
 
+    def prepare(self):
+        """Lay out the flat buffers (first call) and refresh the chunk tables when the set of
+        parameters with a gradient changed. Returns the active flags."""
+        if self.flat_param is None:
+            self._flatten({id(p) for s in self._segments for p in s if p.grad is not None})
+        active = self.current_active()
+        if active != self._active:
+            self._set_active(active)
+        return active
+
     def gather_grads(self):
         """Copy this step's gradients into the flat gradient (once per step) and point p.grad at
         their flat views. Gradients already living in their views (a captured step that keeps
-        them persistent) are not copied."""
-        if self.flat_param is None:
-            self._flatten()
+        them persistent, or engine/dp.py's bucket copies) are not copied."""
+        active = self.prepare()
         if self._gathered:
             return
         dst, src = [], []
-        for p, v in zip(self.flat_params_list, self._gviews):
+        for p, v, a in zip(self.params_all, self._gviews, active):
+            if not a:
+                continue
             g = p.grad
-            if g is None:
-                v.zero_()
-            elif g.data_ptr() != v.data_ptr():
+            if g.data_ptr() != v.data_ptr():
                 dst.append(v)
                 src.append(g)
             p.grad = v
         if dst:
             torch._foreach_copy_(dst, src)
+        self._gathered = True
+
+    def mark_gathered(self):
+        """The caller has placed every active gradient in its flat view already."""
+        for p, v, a in zip(self.params_all, self._gviews, self._active):
+            if a:
+                p.grad = v
         self._gathered = True
 
     # ---- torch.optim.Optimizer API ------------------------------------------------------
@@ -133,9 +209,9 @@ class FlatAdam(torch.optim.Optimizer):
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         _lib.call("ured_adam_clip_step", _p(self.flat_param), _p(self.flat_grad), _p(self.exp_avg),
-                  _p(self.exp_avg_sq), _p(self._cbeg), _p(self._cend), _p(self._cseg), int(self._nchunks),
-                  _p(self._seg0), int(self._nseg), float(max_norm), _p(self._lr_t), _p(self._step_t),
-                  float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), _p(self._partial),
-                  _p(self._coef), _lib.stream_of(self.flat_param))
+                  _p(self.exp_avg_sq), _p(self._cbeg), _p(self._cend), _p(self._cseg), _p(self._cpar),
+                  int(self._nchunks), _p(self._seg0), int(self._nseg), float(max_norm), _p(self._lr_t),
+                  _p(self._pstep), _p(self._act), int(self._nact), float(b1), float(b2), float(g["eps"]),
+                  float(g["weight_decay"]), _p(self._partial), _p(self._coef), _lib.stream_of(self.flat_param))
         self._gathered = False
         return loss

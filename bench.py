@@ -1,6 +1,11 @@
 """U-RED training-step benchmark on MI355X (BASELINE.json metric, config 2 by default).
 
-  python bench.py [--gpus N --steps K --warmup W]      (N>1: launched by torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W]
+
+N > 1: under torch.distributed.run (WORLD_SIZE set) each process is one rank; without it,
+bench.py launches the N ranks itself (a torch.distributed.run child process, started before
+anything touches the GPU) after checking that N GPUs are visible, and exits with its status.
+n_gpus in the JSON line is dist.get_world_size().
 
 A step = one full U-RED training iteration (engine/train.py:196-345): source +
 target encoders, part pooling, 3 residual nets, DeformNet, get_shape, chamfer /
@@ -12,6 +17,8 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,7 +44,7 @@ def workload_cfg(args):
     with open(os.path.join(ge.PKG_DIR, "config", "config_train_test.json")) as f:
         cfg = json.load(f)
     cfg.update({"batch_size": args.batch, "num_points": args.points, "parts": args.parts,
-                "num_source": args.sources, "device": "cuda", "log_every": 0,
+                "num_source": args.sources, "device": "cuda", "log_every": 0, "compute_connectivity": False,
                 "flat_adam": os.environ.get("URED_FLAT_ADAM", "1") == "1"})   # A/B knob: torch's Adam
     return cfg
 
@@ -318,6 +325,60 @@ def pair_rate(dev, parts=512, pts=1024):
             "pairs_per_s": round(npairs / t, 1), "gpair_dist_s": round(npairs * pts * pts / t / 1e9, 1)}
 
 
+def _free_port():
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N` without torch.distributed.run: start the N ranks as a child process (nothing in
+    this process has initialised the GPU: torch.cuda.device_count() does not on this image)."""
+    if not args.cpu_dry_run:
+        n = torch.cuda.device_count()
+        if n < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {n} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args):
+    """--cpu-dry-run: the launcher and the rank bookkeeping of the JSON line without a GPU (gloo;
+    each "step" is an all_reduce of a 1 M-float buffer). For the CPU tests only."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    rank = dist.get_rank() if world > 1 else 0
+    buf = torch.ones(1 << 20)
+    for _ in range(args.warmup):
+        if world > 1:
+            dist.all_reduce(buf)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if world > 1:
+            dist.all_reduce(buf)
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        el = float(t.item())
+        print(json.dumps({"metric": "cpu dry run (launcher check, no GPU work)", "value": args.steps * world / el,
+                          "unit": "iters/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": el / args.steps * 1e3, "dry_run": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -349,14 +410,24 @@ def main():
                     help="skip the chamfer / pseudo-label side measurements (step-only profiles)")
     ap.add_argument("--no-all-slots-rate", action="store_true",
                     help="skip the extra timed run that encodes every source slot")
+    ap.add_argument("--no-k16-rate", action="store_true",
+                    help="skip the extra timed run at 16 parts per target (no padding slots)")
+    ap.add_argument("--cpu-dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.cpu_dry_run:
+        return dry_run(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world, rank = dist.get_world_size(), dist.get_rank()
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: running {world} rank(s) (--gpus {args.gpus})", file=sys.stderr)
     dev = torch.device("cuda", local)
     torch.manual_seed(1234 + rank)
 
@@ -418,15 +489,16 @@ def main():
     elapsed = float(t.item())
     loss_val = float(T["all_loss"].item())
 
-    def timed_rate(steps):   # same protocol (barrier + sync both sides, max over ranks)
+    def timed_rate(steps, bs=None):   # same protocol (barrier + sync both sides, max over ranks)
+        bs = bs or batches
         for i in range(2):
-            eager.step(batches[i % 4])
+            eager.step(bs[i % len(bs)])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
         for i in range(steps):
-            eager.step(batches[i % 4])
+            eager.step(bs[i % len(bs)])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -440,6 +512,14 @@ def main():
         cfg["unique_sources"] = False      # every one of the B x 16 source slots encoded
         all_slots_rate = timed_rate(args.steps)
         cfg["unique_sources"] = True
+    k16_rate = None
+    if not args.no_k16_rate and args.parts != 16:
+        # SURVEY §8(d)'s stress case: 16 parts per target, no padding slots (~200 distinct sources)
+        b16 = [batch_to_device(synthetic.make_batch(args.batch, args.points, db.num_sources, parts=16,
+                                                    seed=5000 + 1000 * rank + i), dev, db.num_sources)
+               for i in range(4)]
+        k16_rate = timed_rate(args.steps, b16)
+        del b16
 
     breakdown = None
     if not args.no_breakdown:
@@ -521,6 +601,8 @@ def main():
                                   for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
     if all_slots_rate is not None:
         extra["all_slots_iters_s"] = round(all_slots_rate, 4)
+    if k16_rate is not None:
+        extra["k16_iters_s"] = round(k16_rate, 4)
     extra["unique_sources"] = bool(cfg["unique_sources"])
     if not args.no_extras:
         ch = chamfer_rate(dev)
@@ -532,7 +614,7 @@ def main():
         extra["inference"] = inference_rate(cfg, db, dev)
         extra["emd"] = emd_rate(dev)
     extra["loss"] = loss_val
-    cpu = None if args.no_cpu_baseline else cpu_baseline(args)
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)   # rank 0 at N=1 only
     out = {"metric": "train iters/sec chair bs=16 2048-pt @1/2/4/8 GPU; Chamfer Gpair-dist/s",
            "value": round(iters_per_s * world, 4), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",

@@ -37,7 +37,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 2
+#define URED_ABI_VERSION 3
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
@@ -200,14 +200,18 @@ int ured_gemm(const UredGemmDesc* d, void* stream);
 /* Optimizer tail of the training step (reference engine/train.py:331-346: clip_grad_norm_(5.0)
  * per module, then torch.optim.Adam with L2 weight decay, train_utils/optimizer_dm.py:68-104)
  * over flat buffers param/grad/exp_avg/exp_avg_sq. Chunk c covers [chunk_beg[c], chunk_end[c])
- * (16-B aligned, lengths multiples of 4) of module segment chunk_seg[c]; segment s owns chunks
- * [seg_chunk0[s], seg_chunk0[s+1]). max_norm > 0: per-segment L2 norm (fp64 chunk partials in
+ * (16-B aligned, lengths multiples of 4) of parameter chunk_param[c] in module segment
+ * chunk_seg[c]; segment s owns chunks [seg_chunk0[s], seg_chunk0[s+1]). Only the chunks of the
+ * parameters that take this step are listed (those with a gradient: torch's clip_grad_norm_
+ * and Adam skip the others). max_norm > 0: per-segment L2 norm (fp64 chunk partials in
  * `partial`, fixed order) -> coef[s] = min(max_norm / (norm + 1e-6), 1), gradient scaled in
- * place; max_norm <= 0: no clipping. *step (device) is incremented, then every element takes
- * one Adam step with *lr (device). Deterministic. */
+ * place; max_norm <= 0: no clipping. param_step[active_params[i]] (device, one step count per
+ * parameter as in torch's Adam) is incremented for i < n_active, then every listed element takes
+ * one Adam step with *lr (device) and its parameter's bias corrections. Deterministic. */
 int ured_adam_clip_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq,
-                        const long long* chunk_beg, const long long* chunk_end, const int* chunk_seg, int nchunks,
-                        const int* seg_chunk0, int nseg, float max_norm, const float* lr, float* step,
+                        const long long* chunk_beg, const long long* chunk_end, const int* chunk_seg,
+                        const int* chunk_param, int nchunks, const int* seg_chunk0, int nseg, float max_norm,
+                        const float* lr, float* param_step, const int* active_params, int n_active,
                         double beta1, double beta2, double eps, double weight_decay, double* partial, float* coef,
                         void* stream);
 

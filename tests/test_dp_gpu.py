@@ -1,7 +1,10 @@
 """DataParallelStep end to end on the GPU box: 2 ranks (gloo — RCCL needs one GPU per rank
 and the test box has one) each run the real HIP train step on its own shard; after
 reduce_gradients every rank must hold the average of the ranks' local gradients, the
-ranks' parameters stay identical after the Adam step."""
+ranks' parameters stay identical after the Adam step. Then four full DataParallelSteps
+(epochs 0, 0, 1, 1 with init_p_m_loss = 0: re_residual_net_full joins at epoch 1) with the
+all-reduce buckets issued from backward's gradient hooks must leave exactly (bitwise) the
+parameters of the same steps with the reduction done after backward."""
 import os
 import socket
 
@@ -68,6 +71,24 @@ def _worker(rank, world, port, q):
         allw = [torch.empty_like(w) for _ in range(world)]
         dist.all_gather(allw, w)
         res["same_params"] = bool(torch.equal(allw[0], allw[1]))
+        cfg = dict(CFG, init_p_m_loss=0)
+        sa = DataParallelStep(cfg, db, dev, bucket_mb=0.2)   # overlapped (default for world > 1)
+        sb = DataParallelStep(cfg, db, dev, overlap=False)
+        for s_ in (sa, sb):
+            for name, sd in ured_ref.make_params(CFG, seed=7).items():
+                s_.models[name].load_state_dict(sd, strict=True)
+        launched = []
+        for ep in (0, 0, 1, 1):
+            sa.step(batch, ep)
+            sb.step(batch, ep)
+            launched.append(sa.reducer.num_buckets)
+        same = True
+        for name in sa.models:
+            pb = dict(sb.models[name].named_parameters())
+            for k, p in sa.models[name].named_parameters():
+                same &= bool(torch.equal(p.detach(), pb[k].detach()))
+        res["overlap_equal"] = same
+        res["buckets"] = launched
         torch.cuda.synchronize()
     finally:
         q.put(res)
@@ -87,3 +108,5 @@ def test_dp_two_ranks_one_gpu(dev):
     for r in res:
         assert r["avg"], r
         assert r["same_params"], r
+        assert r["overlap_equal"], r
+        assert all(n > 1 for n in r["buckets"]), r

@@ -51,8 +51,8 @@ def test_graph_replay_unique_sources_equals_eager(dev):
     parts = [[3, 2], [5, 4], [3, 2], [5, 4], [2, 2]]
     batches = [batch_to_device(synthetic.make_batch(2, 128, 24, parts=p, seed=70 + i), dev, 24, bucket=4)
                for i, p in enumerate(parts)]
-    keys = {GraphedStep.key(b) for b in batches}
-    assert len(keys) >= 2 and None not in keys
+    keys = {b["src_unique"].U for b in batches}
+    assert len(keys) >= 2
     a, b = _make(dev, cfg), _make(dev, cfg)
     g = GraphedStep(a)
     for i in range(2):
@@ -88,3 +88,31 @@ def test_padded_unique_rows_match_unpadded(dev):
         if pa.grad is None:
             continue
         assert (pa.grad - pb.grad).norm() <= 1e-4 * pb.grad.norm() + 1e-6, k
+
+
+def test_graph_replay_across_residual_gate(dev):
+    """init_p_m_loss = 0: the residual loss switches on at epoch 1 (engine/train.py:306-316). The
+    graphs captured at epoch 0 must not be replayed afterwards (the gate is part of the key; the
+    set of parameters with a gradient changes, so everything is re-captured): graph steps equal
+    eager steps bitwise across the flip, and the residual net trains only from epoch 1."""
+    from dataset import synthetic
+    from engine.graph import GraphedStep
+    from engine.train import batch_to_device
+    cfg = dict(CFG, cuda_graph=True, init_p_m_loss=0)
+    batches = [batch_to_device(synthetic.make_batch(2, 128, 24, parts=[3, 2], seed=60 + i), dev) for i in range(3)]
+    a, b = _make(dev, cfg), _make(dev, cfg)
+    g = GraphedStep(a)
+    r0 = {k: p.detach().clone() for k, p in a.models["re_residual_net_full"].named_parameters()}
+    for ep, i in ((0, 0), (0, 1), (0, 2), (1, 0), (1, 1), (1, 2), (1, 0)):
+        Ta = g.step(batches[i], epoch=ep)
+        Tb = b.step(batches[i], epoch=ep)
+        assert torch.equal(Ta["all_loss"], Tb["all_loss"]), (ep, i)
+        assert ("re_reg_loss_full" in Ta) == (ep >= 1)
+        if ep == 0:
+            for k, p in a.models["re_residual_net_full"].named_parameters():
+                assert torch.equal(p.detach(), r0[k]), k
+    assert not torch.equal(a.models["re_residual_net_full"].residual_net[0].weight.detach(),
+                           r0["residual_net.0.weight"])
+    for name in a.models:
+        for (k, pa), (_, pb) in zip(a.models[name].state_dict().items(), b.models[name].state_dict().items()):
+            assert torch.equal(pa, pb), (name, k)

@@ -98,3 +98,35 @@ def test_pickles_end_to_end(dev, tmp_path):
     from ured_hip.nn import dcd
     np.testing.assert_array_equal(torch.stack(dcd(d1, i1, d2, i2)).squeeze(1).cpu().numpy(),
                                   table[:, 7, 5].cpu().numpy())
+
+
+def _golden():
+    import os
+    from conftest import GOLDEN
+    return np.load(os.path.join(GOLDEN, "pseudo_labels.npz"))
+
+
+def test_oracle_matches_reference_golden():
+    """oracle/pseudo_label_ref.py vs the reference's own get_labels / mask_label /
+    check_similarity / read_pickle_topk (tests/golden/make_golden.py golden_pseudo_labels:
+    lifted from dataset/dataset_utils.py:1043-1143, pickle reads from an in-memory table)."""
+    g = _golden()
+    rows = g["part_rows"]
+    lists = [[int(r) for r in row if r >= 0] for row in rows]
+    exp = ref.get_labels(lists, g["cd_m"], g["part_sem"], g["sources_sem"], g["dist_src"], float(g["alpha"]),
+                         int(g["cl_k"]), rows.shape[1])
+    np.testing.assert_array_equal(exp, g["source_labels"])
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_table_matches_reference_golden(device, request):
+    """PseudoLabelTable (the device path that replaces the per-iteration pickle reads) vs the
+    reference's get_labels on the same table: integer labels bit-exact."""
+    from train_utils.pseudo_labels import PseudoLabelTable
+    if device == "cuda":
+        device = request.getfixturevalue("dev")
+    g = _golden()
+    tab = PseudoLabelTable(g["cd_m"], g["part_sem"], g["sources_sem"], g["dist_src"], alpha=float(g["alpha"]),
+                           cl_k=int(g["cl_k"]), device=device)
+    got = tab.labels(torch.from_numpy(g["part_rows"]).to(device)).cpu().numpy()
+    np.testing.assert_array_equal(got, g["source_labels"])

@@ -205,6 +205,64 @@ def test_flat_adam_matches_torch_adam(dev):
     assert fa.flat_grad is not None and pa[0].data_ptr() == fa.flat_param.data_ptr()
 
 
+def test_flat_adam_parameter_set_changes(dev):
+    """Parameters whose gradient appears later (p2 from step 2: the residual net once
+    epoch > init_p_m_loss) or disappears (p4 after step 2) follow torch's Adam exactly: no update
+    while they have no gradient (no weight decay, no moment decay) and a per-parameter step count
+    (bias corrections restart from 1 for a parameter that joins late)."""
+    from ured_hip.optim import FlatAdam
+    g = torch.Generator().manual_seed(5)
+    shapes = [(64, 3), (64,), (128, 64), (5,), (1024, 33), (7, 7)]
+    base = [torch.randn(*s, generator=g) for s in shapes]
+    pa = [torch.nn.Parameter(b.clone().to(dev)) for b in base]
+    pb = [torch.nn.Parameter(b.clone().to(dev)) for b in base]
+    fa = FlatAdam(pa, [pa[:3], pa[3:]], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=5e-4)
+    ta = torch.optim.Adam(pb, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=5e-4, fused=True)
+    for it in range(6):
+        live = [0, 1, 3, 5] + ([2] if it >= 2 else []) + ([4] if it < 2 else [])
+        fa.zero_grad()
+        ta.zero_grad()
+        for i in live:
+            gr = torch.randn(*shapes[i], generator=g).to(dev)
+            pa[i].grad = gr.clone()
+            pb[i].grad = gr.clone()
+        fa.step(max_norm=0.0)
+        ta.step()
+        for i in range(len(shapes)):
+            torch.testing.assert_close(pa[i].detach(), pb[i].detach(), rtol=1e-6, atol=1e-7, msg=f"step {it} p{i}")
+        for i in range(len(shapes)):
+            assert (pa[i].grad is None) == (i not in live), (it, i)
+
+
+def test_residual_net_joins_after_init_p_m_loss(dev):
+    """init_p_m_loss = 0: the residual loss (and so re_residual_net_full's gradient) is off at
+    epoch 0 and on from epoch 1 (engine/train.py:306-316). FlatAdam must leave the residual net
+    untouched at epoch 0 and train it from epoch 1, matching torch's Adam on the first step it
+    takes part in."""
+    ts1, batch = _setup(dev, flat_adam=True, init_p_m_loss=0)[:2]
+    ts2 = _setup(dev, flat_adam=False, init_p_m_loss=0)[0]
+    res0 = {k: p.detach().clone() for k, p in ts1.models["re_residual_net_full"].named_parameters()}
+    for ep in (0, 0):
+        ts1.step(batch, epoch=ep)
+        ts2.step(batch, epoch=ep)
+    for k, p in ts1.models["re_residual_net_full"].named_parameters():
+        assert torch.equal(p.detach(), res0[k]), k
+    before = {k: p.detach().clone() for k, p in ts2.models["re_residual_net_full"].named_parameters()}
+    T1, T2 = ts1.step(batch, epoch=1), ts2.step(batch, epoch=1)
+    assert "re_reg_loss_full" in T1
+    a, b = T1["all_loss"].item(), T2["all_loss"].item()
+    # two steps of Adam amplify last-bit differences of the BN-fed biases (see the test above)
+    assert abs(a - b) <= 1e-4 * abs(b) + 1e-7, (a, b)
+    p2 = dict(ts2.models["re_residual_net_full"].named_parameters())
+    move = max((p2[k].detach() - before[k]).abs().max().item() for k in p2)
+    assert move > 1e-4
+    for k, p in ts1.models["re_residual_net_full"].named_parameters():
+        # Adam's first step moves each element by ~ +-lr (m/sqrt(v) = sign(g)): the two runs
+        # agree except where a tiny gradient's sign differs between the fp32 summation orders
+        d = (p.detach() - p2[k].detach()).abs()
+        assert (d > 0.5 * move).float().mean().item() <= 1e-2, (k, d.max().item(), move)
+
+
 def test_flat_adam_train_steps_match_torch_adam(dev):
     """Full training steps with FlatAdam vs torch's Adam + the one-launch clip. After one step
     the parameters agree to 1e-3 of the step's largest move (the clip factors differ in the last
