@@ -55,10 +55,24 @@ def algo_bytes(M, N, K, epi):
     return 4.0 * (M * K + K * N + M * N) + (4.0 * M * N if epi == 2 else 0.0)
 
 
-def variant_key(kw):
+def variant_key(kw, M=None, N=None, K=None):
+    """The kernel a kernels.gemm call launches (the name rocprof reports): the K <= 4 edge layers
+    go to the streaming kernels (ured_gemm's fwd_small_ok / dgrad_small_ok), the rest to a
+    gemm2_kernel template instance; None for an outer few-tile call that kernels.gemm splits
+    into an EPI_SPLITK launch (+ reduce), which is timed on its own."""
     tf = {False: "false", True: "true"}
-    return (f"gemm2_kernel<{tf[bool(kw.get('a_kmajor', False))]}, {tf[bool(kw.get('b_kmajor', False))]}, "
-            f"{kw.get('pro_a', 0)}, {kw.get('pro_b', 0)}, {kw.get('epi', 0)}>")
+    ak, bk = bool(kw.get("a_kmajor", False)), bool(kw.get("b_kmajor", False))
+    pa, pb, epi = kw.get("pro_a", 0), kw.get("pro_b", 0), kw.get("epi", 0)
+    if K is not None:
+        raw = pa == 0 and pb == 0 and not ak and kw.get("A2") is None and 1 <= K <= 4 and 1 <= N <= 256
+        if raw and epi == 2 and bk and kw.get("pool_idx") is None:
+            return f"dgrad_small_bnbwd_kernel<{K}>"
+        if raw and epi == 1 and not bk and kw.get("pool_ws") is None and kw.get("rowbias") is None:
+            return f"fwd_small_stats_kernel<{K}>"
+        if (epi == 0 and pa == 0 and pb == 0 and kw.get("A2") is None and not ak and K >= 512
+                and ((M + 127) // 128) * ((N + 127) // 128) <= 16):
+            return None
+    return f"gemm2_kernel<{tf[ak]}, {tf[bk]}, {pa}, {pb}, {epi}>"
 
 
 class DominantTimer:
@@ -74,7 +88,7 @@ class DominantTimer:
         rec, key, orig = self.rec, self.key, self.orig
 
         def timed(M, N, K, *a, **kw):
-            if variant_key(kw) != key:
+            if variant_key(kw, M, N, K) != key:
                 return orig(M, N, K, *a, **kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -109,11 +123,14 @@ class GemmTimer:
         rec = self.rec
 
         def timed(M, N, K, *a, **kw):
+            name = variant_key(kw, M, N, K)
+            if name is None:        # split into an EPI_SPLITK launch (timed itself) + reduce
+                return self.orig(M, N, K, *a, **kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             self.orig(M, N, K, *a, **kw)
             e1.record()
-            rec.append((kw.get("epi", 0), kw.get("a_kmajor", False), kw.get("b_kmajor", False),
+            rec.append((name, kw.get("epi", 0), kw.get("a_kmajor", False), kw.get("b_kmajor", False),
                         kw.get("pro_a", 0), kw.get("pro_b", 0), int(M), int(N), int(K), e0, e1))
         kernels.gemm = timed
         return self
@@ -124,8 +141,7 @@ class GemmTimer:
     def summary(self):
         torch.cuda.synchronize()
         by = {}
-        for epi, ak, bk, pa, pb, M, N, K, e0, e1 in self.rec:
-            key = variant_key({"a_kmajor": ak, "b_kmajor": bk, "pro_a": pa, "pro_b": pb, "epi": epi})
+        for key, epi, ak, bk, pa, pb, M, N, K, e0, e1 in self.rec:
             ms = e0.elapsed_time(e1)
             d = by.setdefault(key, {"launches": 0, "ms": 0.0, "flop": 0.0, "bytes": 0.0})
             d["launches"] += 1
@@ -137,8 +153,8 @@ class GemmTimer:
     def shapes(self, steps=1):
         torch.cuda.synchronize()
         by = {}
-        for epi, ak, bk, pa, pb, M, N, K, e0, e1 in self.rec:
-            key = f"epi{epi} akm{int(bool(ak))} bkm{int(bool(bk))} pa{pa} pb{pb} M{M} N{N} K{K}"
+        for name, epi, ak, bk, pa, pb, M, N, K, e0, e1 in self.rec:
+            key = f"{name.split('<')[0]} epi{epi} akm{int(bool(ak))} bkm{int(bool(bk))} pa{pa} pb{pb} M{M} N{N} K{K}"
             d = by.setdefault(key, {"launches": 0, "ms": 0.0})
             d["launches"] += 1
             d["ms"] += e0.elapsed_time(e1)
