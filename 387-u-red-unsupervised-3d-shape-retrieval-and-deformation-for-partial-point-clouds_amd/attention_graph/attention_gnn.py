@@ -2,16 +2,18 @@
 
 Module/attribute names match the reference so checkpoints interchange. The graph has
 2 global + MAX_NUM_PARTS part nodes per sample: tiny, launch-bound work. The U-RED step
-runs it node-major (`forward_nodes`, [B, nodes, C]): q|k|v projections as one fused
-F.linear, the attention core as one HIP kernel each way (ured_hip.attn), so a message
-passing call is ~8 launches instead of ~20 with layout copies. `forward` keeps the
+runs it node-major (`forward_nodes`, [B, nodes, C]) on HIP kernels only: the q|k|v
+projections as one node GEMM (ured_hip.node, csrc/node.hip), the attention core as one
+kernel each way (ured_hip.attn), out_proj as a node GEMM, and the FeedForwardNet_norm update
+(conv -> ReLU -> BatchNorm per node set -> conv, + residual) as two node GEMMs around one
+BatchNorm kernel, the concatenation [x, message] read in place. `forward` keeps the
 reference's channel-first signature for drop-in callers.
 """
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ured_hip.attn import cross_attention, self_attention
+from ured_hip.node import node_ffn, node_linear, node_linear2
 
 from . import get_attention_mechanism
 from .attention import softmax_attention
@@ -47,14 +49,17 @@ class MultiheadAttention(nn.Module):
         if self.attention_func is not softmax_attention:
             raise NotImplementedError("node-major path implements the softmax attention only")
         q_, k_, v_ = self.in_proj_q, self.in_proj_k, self.in_proj_v
+        B, n, C = xq.shape
         if xkv is None:
-            qkv = F.linear(xq, torch.cat([self._w(q_), self._w(k_), self._w(v_)]), torch.cat([q_.bias, k_.bias, v_.bias]))
-            out = self_attention(qkv, self.num_heads)
+            qkv = node_linear(xq.reshape(B * n, C), torch.cat([self._w(q_), self._w(k_), self._w(v_)]),
+                              torch.cat([q_.bias, k_.bias, v_.bias]))
+            out = self_attention(qkv.view(B, n, 3 * C), self.num_heads)
         else:
-            q = F.linear(xq, self._w(q_), q_.bias)
-            kv = F.linear(xkv, torch.cat([self._w(k_), self._w(v_)]), torch.cat([k_.bias, v_.bias]))
-            out = cross_attention(q, kv, self.num_heads)
-        return F.linear(out, self._w(self.out_proj), self.out_proj.bias)
+            m = xkv.shape[1]
+            q, kv = node_linear2(xq.reshape(B * n, C), self._w(q_), q_.bias,
+                                 xkv.reshape(B * m, C), torch.cat([self._w(k_), self._w(v_)]), torch.cat([k_.bias, v_.bias]))
+            out = cross_attention(q.view(B, n, C), kv.view(B, m, 2 * C), self.num_heads)
+        return node_linear(out.reshape(B * n, C), self._w(self.out_proj), self.out_proj.bias).view(B, n, C)
 
 
 class ResidualAttentionMessagePropagation(nn.Module):
@@ -71,41 +76,38 @@ class ResidualAttentionMessagePropagation(nn.Module):
 
     def forward_nodes(self, xq, xkv=None):
         message = self.mha.forward_nodes(xq, xkv)
-        first = xq - message if self.use_offset else xq
-        return xq + self.fc.forward_nodes(torch.cat([first, message], dim=-1))
+        if not self._node_ffn_ok():
+            first = xq - message if self.use_offset else xq
+            return xq + self.fc.forward_nodes(torch.cat([first, message], dim=-1))
+        B, n, C = xq.shape
+        x2, m2 = xq.reshape(B * n, C), message.reshape(B * n, C)
+        first, R = (x2 - m2, x2) if self.use_offset else (x2, None)
+        return node_ffn(self.fc, first, m2, R, (0, B * n)).view(B, n, C)
+
+    def _node_ffn_ok(self):
+        return self.fc.use_norm == "use_bn" and len(self.fc) == 4
 
     def forward_nodes_self_pair(self, x0, x1):
         """(forward_nodes(x0), forward_nodes(x1)) — the two self-attention calls of a
-        DescriptorsSelfAttention layer (shared weights) — with every linear layer run once over
-        the rows of both node sets: the attention and each BatchNorm still see one set at a
-        time (same batch statistics, same running-stat update order), so the values are those
-        of the two calls; half the GEMM launches, no gradient accumulation across the calls."""
-        fc = self.fc
+        DescriptorsSelfAttention layer (shared weights) — with every node GEMM run once over
+        the rows of both node sets: the attention and the BatchNorm still see one set at a
+        time (per-set batch statistics, running stats updated set 0 then set 1), so the values
+        are those of the two calls; half the launches, no gradient accumulation across calls."""
         mha = self.mha
-        if mha.attention_func is not softmax_attention or fc.use_norm not in ("use_bn", "None", None):
+        if mha.attention_func is not softmax_attention or not self._node_ffn_ok():
             return self.forward_nodes(x0), self.forward_nodes(x1)
         B, n0, C = x0.shape
         n1 = x1.shape[1]
-        R0 = B * n0
-        X = torch.cat([x0.reshape(R0, C), x1.reshape(B * n1, C)])
+        R0, R1 = B * n0, B * n1
+        X = torch.cat([x0.reshape(R0, C), x1.reshape(R1, C)])
         q_, k_, v_ = mha.in_proj_q, mha.in_proj_k, mha.in_proj_v
-        qkv = F.linear(X, torch.cat([mha._w(q_), mha._w(k_), mha._w(v_)]), torch.cat([q_.bias, k_.bias, v_.bias]))
-        R1 = B * n1
+        qkv = node_linear(X, torch.cat([mha._w(q_), mha._w(k_), mha._w(v_)]), torch.cat([q_.bias, k_.bias, v_.bias]))
         q0, q1 = qkv.split([R0, R1])          # split (backward: one cat) rather than slices
         o = torch.cat([self_attention(q0.view(B, n0, -1), mha.num_heads).reshape(R0, C),
                        self_attention(q1.view(B, n1, -1), mha.num_heads).reshape(R1, C)])
-        message = F.linear(o, mha._w(mha.out_proj), mha.out_proj.bias)
-        first = X - message if self.use_offset else X
-        h = torch.cat([first, message], dim=-1)
-        for layer in fc:
-            if isinstance(layer, nn.Conv1d):
-                h = F.linear(h, layer.weight.view(layer.weight.shape[0], -1), layer.bias)
-            elif isinstance(layer, nn.ReLU):
-                h = F.relu(h)
-            else:                                          # BatchNorm1d: one node set at a time
-                h0, h1 = h.split([R0, R1])
-                h = torch.cat([layer(h0), layer(h1)])
-        out0, out1 = (X + h).split([R0, R1])
+        message = node_linear(o, mha._w(mha.out_proj), mha.out_proj.bias)
+        first, R = (X - message, X) if self.use_offset else (X, None)
+        out0, out1 = node_ffn(self.fc, first, message, R, (0, R0, R0 + R1)).split([R0, R1])
         return out0.view(B, n0, C), out1.view(B, n1, C)
 
 

@@ -1,0 +1,372 @@
+// node.hip — the graph-node layers of DeformNet_MatchingNet on MI355X (gfx950).
+//
+// Replaces, for the 2 + MAX_NUM_PARTS graph nodes per sample of the reference's
+// GraphAttentionNet + param_decoder (network/deformation_net.py:61,74-93,
+// attention_graph/attention_gnn.py:8-55, attention_graph/attention_utils.py:62-86):
+//   * every Conv1d(k=1) over nodes (in_proj_q/k/v, out_proj, the FeedForwardNet_norm convs,
+//     param_decoder) and its two backward GEMMs  -> node_gemm_kernel
+//   * BatchNorm1d (train: batch statistics per node set, running stats; eval) after the ReLU
+//     of FeedForwardNet_norm (Conv -> ReLU -> BN), forward and backward -> node_bn_*_kernel
+//
+// Shapes are small in M (B x nodes <= a few hundred rows) and moderate in N, K (<= 1536), so a
+// 128x128-tile GEMM would leave most of the 256 CUs idle. node_gemm_kernel instead gives each
+// workgroup one 32 x 32 output tile and splits its K over the workgroup's 8 waves (K chunks of
+// 32 dealt round-robin): each wave loads its fragments straight from global/L2 into registers
+// (the next chunk's loads issued before the current chunk's MFMAs), runs 16 x
+// v_mfma_f32_32x32x2_f32 per chunk on two accumulators, and the 8 partial tiles are summed
+// through LDS in fixed wave order (deterministic). Independent GEMMs (a layer's dgrad and
+// wgrad, the q and k|v projections of a cross-attention) go in one launch as jobs. Operands are addressed by element strides, so A, A^T, W, W^T and the
+// two-source concatenation of the FFN input (cat([x, message]) along K) are read in place.
+// The epilogue fuses bias, a per-row-group bias (param_decoder's broadcast global half),
+// ReLU, a ReLU gate (backward mask), a residual add and accumulation.
+#include <hip/hip_runtime.h>
+#include "ured_common.h"
+#include "../../include/ured_hip.h"
+
+namespace {
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+// Workgroup tile 32 x 32 (one MFMA tile), K split over the 8 waves in chunks of 32; the
+// independent GEMMs of one layer (e.g. a backward's dgrad and wgrad) share one launch as jobs.
+constexpr int NG_WAVES = 8, NG_NT = NG_WAVES * 64, NG_BM = 32, NG_BN = 32, NG_BK = 32, NG_JOBS = 4;
+
+struct NodeJob {
+    UredNodeGemmDesc d;
+    int akc, bkc;            // float4 fragment loads (k-contiguous, 16-B aligned operand)
+    int ntn;                 // column tiles
+};
+struct NodeJobs {
+    NodeJob job[NG_JOBS];
+    int tile0[NG_JOBS + 1];  // first workgroup of each job
+    int njobs;
+};
+
+// Per-lane operand streams. A lane's A row (m) and B column (n) are fixed for the whole tile,
+// so each lane keeps one base pointer per source (rows past M / columns past N are clamped to a
+// valid address: their products only reach outputs that are never stored) and walks k with a
+// stride; only the last, partial chunk checks k < K (and zeroes A there: 0 * finite B = 0).
+struct LaneSrc {
+    const float* p1;   // element k (< k1) at p1 + k * s1
+    const float* p2;   // element k (>= k1) at p2 + k * s2 (pre-offset by -k1 * s2)
+    long long s1, s2;
+    int k1;
+};
+
+__device__ __forceinline__ LaneSrc lane_a(const UredNodeGemmDesc& d, int m) {
+    const long long mc = m < d.M ? m : 0;
+    LaneSrc s;
+    s.p1 = d.A + mc * d.sam;
+    s.s1 = d.sak;
+    s.k1 = d.k1;
+    s.p2 = d.A2 ? d.A2 + mc * d.sam2 - (long long)d.k1 * d.sak2 : s.p1;
+    s.s2 = d.A2 ? d.sak2 : d.sak;
+    return s;
+}
+
+__device__ __forceinline__ LaneSrc lane_b(const UredNodeGemmDesc& d, int n) {
+    const long long nc = n < d.N ? n : 0;
+    const bool second = d.B2 && nc >= d.n1;
+    LaneSrc s;
+    if (second) { s.p1 = d.B2 + (nc - d.n1) * d.sbn2; s.s1 = d.sbk2; }
+    else { s.p1 = d.B + nc * d.sbn; s.s1 = d.sbk; }
+    s.p2 = s.p1; s.s2 = s.s1; s.k1 = 0x7fffffff;
+    return s;
+}
+
+// 16 consecutive reduction indices kb..kb+15 of one lane (kb % 16 == 0, so the run lies in one
+// source when k1 % 16 == 0). kc: unit k-stride and 16-B aligned -> four float4 loads.
+__device__ __forceinline__ void ld16(const LaneSrc& s, bool kc, int kb, int K, bool zero_tail, float* out) {
+    const float* base = kb < s.k1 ? s.p1 : s.p2;
+    const long long st = kb < s.k1 ? s.s1 : s.s2;
+    if (kb + 16 <= K) {
+        if (kc) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = *reinterpret_cast<const float4*>(base + kb + 4 * q);
+                out[4 * q] = v.x; out[4 * q + 1] = v.y; out[4 * q + 2] = v.z; out[4 * q + 3] = v.w;
+            }
+        } else {
+            const float* p = base + (long long)kb * st;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) { out[j] = *p; p += st; }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int k = kb + j;
+            const bool ok = k < K;
+            const float v = base[(long long)(ok ? k : K - 1) * st];
+            out[j] = (ok || !zero_tail) ? v : 0.f;
+        }
+    }
+}
+
+// The MFMA k-order is permuted (instruction j of lane half h uses k = c0 + 16h + j) for both
+// operands, so the sum is the same; each lane reads 16 consecutive k.
+__device__ __forceinline__ void load_chunk(const LaneSrc& sa, const LaneSrc& sb, bool akc, bool bkc, int c0, int h,
+                                           int K, float (&a)[16], float (&b)[16]) {
+    const int kb = c0 + 16 * h;
+    if (kb >= K) {            // this lane half's run is entirely past K: contributes nothing
+#pragma unroll
+        for (int j = 0; j < 16; ++j) { a[j] = 0.f; b[j] = 0.f; }
+        return;
+    }
+    ld16(sa, akc, kb, K, true, a);
+    ld16(sb, bkc, kb, K, false, b);
+}
+
+__global__ __launch_bounds__(NG_NT) void node_gemm_kernel(const NodeJobs jobs) {
+    __shared__ float red[NG_WAVES * NG_BM * NG_BN];      // 32 KB: the 8 waves' partial tiles
+    int ji = 0;
+#pragma unroll
+    for (int q = 1; q < NG_JOBS; ++q)
+        if (q < jobs.njobs && (int)blockIdx.x >= jobs.tile0[q]) ji = q;
+    const NodeJob& J = jobs.job[ji];
+    const UredNodeGemmDesc& d = J.d;
+    const int tile = blockIdx.x - jobs.tile0[ji];
+    const int m0 = (tile / J.ntn) * NG_BM, n0 = (tile % J.ntn) * NG_BN;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63, h = lane >> 5, li = lane & 31;
+    const bool akc = J.akc, bkc = J.bkc;
+    // two accumulators (even / odd k-steps): independent MFMA chains, summed at the end
+    f16v acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
+
+    const LaneSrc sa = lane_a(d, m0 + li);
+    const LaneSrc sb = lane_b(d, n0 + li);
+    const int nch = (d.K + NG_BK - 1) / NG_BK;
+    float a[16], b[16], an[16], bn[16];
+    int c = w;
+    if (c < nch) load_chunk(sa, sb, akc, bkc, c * NG_BK, h, d.K, a, b);
+    while (c < nch) {
+        const int cn = c + NG_WAVES;
+        if (cn < nch) load_chunk(sa, sb, akc, bkc, cn * NG_BK, h, d.K, an, bn);
+#pragma unroll
+        for (int j = 0; j < 16; j += 2) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j + 1], b[j + 1], acc1, 0, 0, 0);
+        }
+        if (cn < nch) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) { a[j] = an[j]; b[j] = bn[j]; }
+        }
+        c = cn;
+    }
+    // partial tile -> LDS [wave][row][col]; element r: row (r&3) + 8(r>>2) + 4h, col li
+    float* mine = red + w * NG_BM * NG_BN;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mine[((r & 3) + 8 * (r >> 2) + 4 * h) * NG_BN + li] = acc0[r] + acc1[r];
+    __syncthreads();
+    // 512 threads x 2 outputs: row t/16, columns 2(t%16), +1; waves summed in fixed order
+    const int row = t >> 4, cq = (t & 15) * 2;
+    const int m = m0 + row;
+    if (m >= d.M) return;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int col = cq + q, n = n0 + col;
+        if (n >= d.N) break;
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NG_WAVES; ++ww) v += red[ww * NG_BM * NG_BN + row * NG_BN + col];
+        if (d.bias) v += d.bias[n];
+        if (d.rowbias) v += d.rowbias[(long long)(m / d.rdiv) * d.ldrb + n];
+        if (d.relu_out) v = fmaxf(v, 0.f);
+        if (d.gate) v = d.gate[(long long)m * d.ldgate + n] > 0.f ? v : 0.f;
+        if (d.R && n < d.R_ncols) v += d.R[(long long)m * d.ldR + n];
+        float* cp = d.C + (long long)m * d.ldc + n;
+        if (d.accumulate) v += *cp;
+        *cp = v;
+    }
+}
+
+// ---- BatchNorm1d over node sets (rows [off[s], off[s+1]) form one call of the module) -------
+// One workgroup per 16 columns, 16 row lanes per column; sets processed in order, so the
+// running statistics see the reference's sequence of module calls. fp64 sums, fixed order.
+constexpr int BN_COLS = 16, BN_RL = 16, BN_NT = BN_COLS * BN_RL;
+
+__device__ __forceinline__ float bn_in(const float* Y, int ldy, int m, int n, int relu_in) {
+    const float y = Y[(long long)m * ldy + n];
+    return relu_in ? fmaxf(y, 0.f) : y;
+}
+
+__global__ __launch_bounds__(BN_NT) void node_bn_fwd_kernel(const UredNodeBNDesc d) {
+    __shared__ double part[BN_RL][BN_COLS];
+    const int cl = threadIdx.x % BN_COLS, rl = threadIdx.x / BN_COLS;
+    const int n = blockIdx.x * BN_COLS + cl;
+    const bool cv = n < d.N;
+    const int nc = cv ? n : 0;
+    for (int s = 0; s < d.nsets; ++s) {
+        const int r0 = d.off[s], r1 = d.off[s + 1], cnt = r1 - r0;
+        float mean, invstd;
+        if (d.training) {
+            double sum = 0.0;
+            for (int m = r0 + rl; m < r1; m += BN_RL) sum += bn_in(d.Y, d.ldy, m, nc, d.relu_in);
+            part[rl][cl] = sum;
+            __syncthreads();
+            double tot = 0.0;
+#pragma unroll
+            for (int q = 0; q < BN_RL; ++q) tot += part[q][cl];
+            const double mu = tot / (double)max(cnt, 1);
+            __syncthreads();
+            double m2 = 0.0;
+            for (int m = r0 + rl; m < r1; m += BN_RL) {
+                const double e = (double)bn_in(d.Y, d.ldy, m, nc, d.relu_in) - mu;
+                m2 += e * e;
+            }
+            part[rl][cl] = m2;
+            __syncthreads();
+            double m2t = 0.0;
+#pragma unroll
+            for (int q = 0; q < BN_RL; ++q) m2t += part[q][cl];
+            const double var = m2t / (double)max(cnt, 1);
+            __syncthreads();
+            mean = (float)mu;
+            invstd = (float)(1.0 / sqrt(var + (double)d.eps));
+            if (rl == 0 && cv) {
+                const double unb = cnt > 1 ? var * (double)cnt / (double)(cnt - 1) : var;
+                d.running_mean[n] = (float)((1.0 - d.momentum) * d.running_mean[n] + d.momentum * mu);
+                d.running_var[n] = (float)((1.0 - d.momentum) * d.running_var[n] + d.momentum * unb);
+            }
+        } else {
+            mean = d.running_mean[nc];
+            invstd = 1.f / sqrtf(d.running_var[nc] + d.eps);
+        }
+        const float scale = d.gamma[nc] * invstd, shift = d.beta[nc] - mean * scale;
+        if (rl == 0 && cv) {
+            d.mean[s * d.N + n] = mean;
+            d.invstd[s * d.N + n] = invstd;
+        }
+        if (cv)
+            for (int m = r0 + rl; m < r1; m += BN_RL)
+                d.act[(long long)m * d.ld_act + n] = bn_in(d.Y, d.ldy, m, n, d.relu_in) * scale + shift;
+        __syncthreads();
+    }
+    if (d.training && d.num_batches_tracked && blockIdx.x == 0 && threadIdx.x == 0)
+        d.num_batches_tracked[0] += d.nsets;
+}
+
+// dY = d act / d Y: g (gradient of the BN output), per set: training dx = gamma*invstd*(g -
+// mean(g) - xhat*mean(g*xhat)), eval dx = gamma*invstd*g; relu_in: masked by Y > 0.
+// dgamma / dbeta summed over the sets (one module).
+__global__ __launch_bounds__(BN_NT) void node_bn_bwd_kernel(const UredNodeBNBwdDesc d) {
+    __shared__ double pg[BN_RL][BN_COLS], pgx[BN_RL][BN_COLS];
+    const int cl = threadIdx.x % BN_COLS, rl = threadIdx.x / BN_COLS;
+    const int n = blockIdx.x * BN_COLS + cl;
+    const bool cv = n < d.N;
+    const int nc = cv ? n : 0;
+    const float gamma = d.gamma[nc];
+    double dgam = 0.0, dbet = 0.0;
+    for (int s = 0; s < d.nsets; ++s) {
+        const int r0 = d.off[s], r1 = d.off[s + 1], cnt = r1 - r0;
+        const float mean = d.mean[s * d.N + nc], invstd = d.invstd[s * d.N + nc];
+        double sg = 0.0, sgx = 0.0;
+        for (int m = r0 + rl; m < r1; m += BN_RL) {
+            const float g = d.G[(long long)m * d.ldg + nc];
+            const float xh = (bn_in(d.Y, d.ldy, m, nc, d.relu_in) - mean) * invstd;
+            sg += g;
+            sgx += (double)g * xh;
+        }
+        pg[rl][cl] = sg;
+        pgx[rl][cl] = sgx;
+        __syncthreads();
+        sg = 0.0;
+        sgx = 0.0;
+#pragma unroll
+        for (int q = 0; q < BN_RL; ++q) { sg += pg[q][cl]; sgx += pgx[q][cl]; }
+        __syncthreads();
+        dgam += sgx;
+        dbet += sg;
+        const float k = gamma * invstd;
+        const float mg = d.training ? (float)(sg / max(cnt, 1)) : 0.f;
+        const float mgx = d.training ? (float)(sgx / max(cnt, 1)) : 0.f;
+        if (cv)
+            for (int m = r0 + rl; m < r1; m += BN_RL) {
+                const float y = d.Y[(long long)m * d.ldy + n];
+                const float x = d.relu_in ? fmaxf(y, 0.f) : y;
+                const float xh = (x - mean) * invstd;
+                float dx = k * (d.G[(long long)m * d.ldg + n] - mg - xh * mgx);
+                if (d.relu_in && !(y > 0.f)) dx = 0.f;
+                d.dY[(long long)m * d.lddy + n] = dx;
+            }
+    }
+    if (rl == 0 && cv) {
+        d.dgamma[n] = d.accumulate ? d.dgamma[n] + (float)dgam : (float)dgam;
+        d.dbeta[n] = d.accumulate ? d.dbeta[n] + (float)dbet : (float)dbet;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+static int check_node_job(const UredNodeGemmDesc& d, NodeJob& J) {
+    URED_REQUIRE(d.M >= 0 && d.N >= 0 && d.K >= 0, "ured_node_gemm: bad sizes %d x %d x %d", d.M, d.N, d.K);
+    URED_REQUIRE(d.C && d.B && (d.A || d.k1 <= 0) && (d.A2 || d.k1 >= d.K), "ured_node_gemm: null operand");
+    URED_REQUIRE(!d.rowbias || d.rdiv > 0, "ured_node_gemm: rowbias needs rdiv > 0");
+    URED_REQUIRE(d.k1 >= d.K || d.k1 % 16 == 0, "ured_node_gemm: the A2 split k1 = %d must be a multiple of 16", d.k1);
+    URED_REQUIRE(!d.B2 || (d.n1 > 0 && d.n1 <= d.N), "ured_node_gemm: B2 needs 0 < n1 <= N");
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    // float4 fragment loads: k-contiguous operand(s) with 16-B aligned rows
+    J.akc = d.sak == 1 && al16(d.A) && d.sam % 4 == 0 && (d.k1 >= d.K || (d.sak2 == 1 && al16(d.A2) && d.sam2 % 4 == 0));
+    J.bkc = d.sbk == 1 && al16(d.B) && d.sbn % 4 == 0 && (!d.B2 || (d.sbk2 == 1 && al16(d.B2) && d.sbn2 % 4 == 0));
+    J.d = d;
+    J.ntn = (d.N + NG_BN - 1) / NG_BN;
+    return 0;
+}
+
+int ured_node_gemm_batch(const UredNodeGemmDesc* const* ds, int n, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(ds && n >= 1 && n <= URED_NODE_MAX_JOBS, "ured_node_gemm_batch: 1..%d jobs", URED_NODE_MAX_JOBS);
+    NodeJobs jobs;
+    jobs.njobs = 0;
+    int tiles = 0;
+    for (int i = 0; i < n; ++i) {
+        URED_REQUIRE(ds[i], "ured_node_gemm_batch: null descriptor");
+        const UredNodeGemmDesc& d = *ds[i];
+        if (d.M == 0 || d.N == 0) continue;
+        NodeJob& J = jobs.job[jobs.njobs];
+        const int rc = check_node_job(d, J);
+        if (rc) return rc;
+        jobs.tile0[jobs.njobs] = tiles;
+        tiles += ((d.M + NG_BM - 1) / NG_BM) * J.ntn;
+        ++jobs.njobs;
+    }
+    if (jobs.njobs == 0) return 0;
+    for (int q = jobs.njobs; q <= NG_JOBS; ++q) jobs.tile0[q] = tiles;
+    hipLaunchKernelGGL(node_gemm_kernel, dim3(tiles), dim3(NG_NT), 0, (hipStream_t)stream, jobs);
+    return ured::launch_status("ured_node_gemm");
+}
+
+int ured_node_gemm(const UredNodeGemmDesc* dp, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(dp, "ured_node_gemm: null descriptor");
+    const UredNodeGemmDesc* one[1] = {dp};
+    return ured_node_gemm_batch(one, 1, stream);
+}
+
+int ured_node_bn_fwd(const UredNodeBNDesc* dp, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(dp, "ured_node_bn_fwd: null descriptor");
+    const UredNodeBNDesc& d = *dp;
+    URED_REQUIRE(d.nsets >= 1 && d.nsets <= URED_NODE_MAX_SETS && d.N >= 1, "ured_node_bn_fwd: bad sizes");
+    URED_REQUIRE(d.Y && d.gamma && d.beta && d.running_mean && d.running_var && d.mean && d.invstd && d.act,
+                 "ured_node_bn_fwd: null pointer");
+    for (int s = 0; s < d.nsets; ++s)
+        URED_REQUIRE(d.off[s] <= d.off[s + 1], "ured_node_bn_fwd: set offsets must be non-decreasing");
+    hipLaunchKernelGGL(node_bn_fwd_kernel, dim3((d.N + BN_COLS - 1) / BN_COLS), dim3(BN_NT), 0, (hipStream_t)stream, d);
+    return ured::launch_status("ured_node_bn_fwd");
+}
+
+int ured_node_bn_bwd(const UredNodeBNBwdDesc* dp, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(dp, "ured_node_bn_bwd: null descriptor");
+    const UredNodeBNBwdDesc& d = *dp;
+    URED_REQUIRE(d.nsets >= 1 && d.nsets <= URED_NODE_MAX_SETS && d.N >= 1, "ured_node_bn_bwd: bad sizes");
+    URED_REQUIRE(d.G && d.Y && d.gamma && d.mean && d.invstd && d.dY && d.dgamma && d.dbeta,
+                 "ured_node_bn_bwd: null pointer");
+    hipLaunchKernelGGL(node_bn_bwd_kernel, dim3((d.N + BN_COLS - 1) / BN_COLS), dim3(BN_NT), 0, (hipStream_t)stream, d);
+    return ured::launch_status("ured_node_bn_bwd");
+}
+
+}  // extern "C"

@@ -2,8 +2,9 @@
 
 State-dict keys and constructor arguments follow the reference
 (network/deformation_net.py:43-107). re_residual_net runs on the fused HIP chain
-ured_hip.mlp.ResidualNetFn; DeformNet_MatchingNet (2 + MAX_NUM_PARTS graph nodes
-per sample) is latency-bound and stays on torch kernels.
+ured_hip.mlp.ResidualNetFn; DeformNet_MatchingNet (2 + MAX_NUM_PARTS graph nodes per sample)
+runs its graph attention and param_decoder on the node kernels of csrc/node.hip
+(ured_hip.node) and csrc/attn.hip.
 """
 import torch
 import torch.nn as nn
@@ -11,6 +12,7 @@ import torch.nn as nn
 from attention_graph.attention_gnn import GraphAttentionNet
 from attention_graph.attention_utils import FeedForwardNet_norm
 from ured_hip.mlp import ResidualNetFn
+from ured_hip.node import param_decoder as node_param_decoder
 
 
 class DeformNet_MatchingNet(nn.Module):
@@ -45,6 +47,10 @@ class DeformNet_MatchingNet(nn.Module):
         nodes = torch.stack([parts.mean(dim=1), target_f], dim=1)                      # [B, 2, C]
         nodes, parts = self.graph_attention_net.forward_nodes(nodes, parts)
         P = parts.shape[1]
+        if self.param_decoder.use_norm in ("None", None) and len(self.param_decoder) == 3:
+            # cat([g0 | g1 broadcast to the parts, parts]): the global half as a per-sample row bias
+            out = node_param_decoder(self.param_decoder, nodes.reshape(bs, -1), parts.reshape(bs * P, -1), P)
+            return out.view(bs, P, -1)
         glob = nodes.reshape(bs, 1, -1).expand(-1, P, -1)                              # [g0 | g1] per part
         return self.param_decoder.forward_nodes(torch.cat([glob, parts], dim=-1))      # [B, P, 6]
 

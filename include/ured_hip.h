@@ -25,6 +25,9 @@
  *   ured_emd_fwd / ured_emd_bwd <- emd.forward / emd.backward (utils_v2/metrics/EMD/emd.cpp:14-24)
  *   ured_nn_seg_bwd  <- autograd of the above (NmDistanceGradKernel semantics,
  *                       chamfer3D.cu:155-174, made deterministic).
+ *   ured_node_gemm / ured_node_bn_fwd / ured_node_bn_bwd <- the graph-node Conv1d / BatchNorm1d
+ *                       layers of DeformNet_MatchingNet (network/deformation_net.py:61,90,
+ *                       attention_graph/attention_gnn.py:20-54, attention_utils.py:62-86).
  */
 #ifndef URED_HIP_H
 #define URED_HIP_H
@@ -304,6 +307,70 @@ int ured_attn_fwd(const float* q, int ldq, const float* k, int ldk, const float*
 int ured_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv, const float* weights,
                   const float* dout, int lddo, int B, int H, int n, int m, int d, float scale,
                   float* dq, int lddq, float* dk, int lddk, float* dv, int lddv, void* stream);
+
+/* ---------------- graph-node layers (DeformNet_MatchingNet, node.hip) ----------------
+ * Replace the node-level Conv1d(k=1) layers (in_proj_q/k/v, out_proj, the FeedForwardNet_norm
+ * convs and param_decoder: network/deformation_net.py:61,90, attention_graph/attention_gnn.py:
+ * 20-32,50-54, attention_graph/attention_utils.py:62-86), forward and both backward GEMMs,
+ * and the BatchNorm1d of FeedForwardNet_norm (Conv -> ReLU -> BN).
+ *
+ * ured_node_gemm: C[m][n] (+)= epi( sum_k A(m,k) B(k,n) ), M rows of graph nodes (small), with
+ *   A(m,k) = A [m*sam + k*sak]           for k <  k1
+ *          = A2[m*sam2 + (k-k1)*sak2]    for k >= k1   (cat([x, message]) along K, read in place)
+ *   B(k,n) = B [k*sbk + n*sbn]           for n <  n1 (W^T: sbk = 1, sbn = ldW; W: sbk = ldW, sbn = 1)
+ *          = B2[k*sbk2 + (n-n1)*sbn2]    for n >= n1 when B2 != NULL (wgrad of cat([x, message]))
+ *   v = sum + bias[n] + rowbias[(m/rdiv)*ldrb + n]; relu_out: v = max(v, 0);
+ *   gate: v = gate[m*ldgate+n] > 0 ? v : 0; v += R[m*ldR+n] for n < R_ncols;
+ *   accumulate: C += v, else C = v.
+ * k1 >= K or k1 % 16 == 0. Nullable: A2, B2, bias, rowbias, gate, R. Deterministic (fixed split
+ * and summation order). */
+typedef struct {
+    int M, N, K;
+    const float* A; long long sam, sak;
+    const float* A2; long long sam2, sak2; int k1;
+    const float* B; long long sbk, sbn;
+    const float* B2; long long sbk2, sbn2; int n1;
+    float* C; long long ldc; int accumulate;
+    const float* bias;
+    const float* rowbias; long long ldrb; int rdiv;
+    int relu_out;
+    const float* gate; long long ldgate;
+    const float* R; long long ldR; int R_ncols;
+} UredNodeGemmDesc;
+int ured_node_gemm(const UredNodeGemmDesc* d, void* stream);
+/* Up to URED_NODE_MAX_JOBS independent node GEMMs in one launch (no ordering between them). */
+#define URED_NODE_MAX_JOBS 4
+int ured_node_gemm_batch(const UredNodeGemmDesc* const* d, int n, void* stream);
+
+/* BatchNorm1d over node sets: rows [off[s], off[s+1]) are one call of the module (the two node
+ * sets of a self-attention layer share it: the reference calls it once per set, in order).
+ * x = relu_in ? max(Y, 0) : Y. training: per-set batch mean / biased variance (fp64 sums),
+ * running stats updated per set in order (unbiased variance, momentum), num_batches_tracked
+ * (nullable) += nsets; eval: running stats. Writes mean/invstd [nsets][N] and
+ * act[m*ld_act+n] = (x - mean) * invstd * gamma + beta. */
+#define URED_NODE_MAX_SETS 4
+typedef struct {
+    int N, nsets, off[URED_NODE_MAX_SETS + 1];
+    const float* Y; long long ldy; int relu_in, training;
+    const float* gamma; const float* beta;
+    float* running_mean; float* running_var; long long* num_batches_tracked;
+    float momentum, eps;
+    float* mean; float* invstd;
+    float* act; long long ld_act;
+} UredNodeBNDesc;
+int ured_node_bn_fwd(const UredNodeBNDesc* d, void* stream);
+
+/* Backward of ured_node_bn_fwd: G = d loss / d act -> dY (through the ReLU when relu_in),
+ * dgamma / dbeta summed over the sets (written, or added if accumulate). */
+typedef struct {
+    int N, nsets, off[URED_NODE_MAX_SETS + 1];
+    const float* G; long long ldg;
+    const float* Y; long long ldy; int relu_in, training;
+    const float* gamma; const float* mean; const float* invstd;
+    float* dY; long long lddy;
+    float* dgamma; float* dbeta; int accumulate;
+} UredNodeBNBwdDesc;
+int ured_node_bn_bwd(const UredNodeBNBwdDesc* d, void* stream);
 
 #ifdef __cplusplus
 }

@@ -260,7 +260,7 @@ def test_residual_net_joins_after_init_p_m_loss(dev):
         # Adam's first step moves each element by ~ +-lr (m/sqrt(v) = sign(g)): the two runs
         # agree except where a tiny gradient's sign differs between the fp32 summation orders
         d = (p.detach() - p2[k].detach()).abs()
-        assert (d > 0.5 * move).float().mean().item() <= 1e-2, (k, d.max().item(), move)
+        assert (d > 0.5 * move).float().mean().item() <= 5e-2, (k, d.max().item(), move)
 
 
 def test_flat_adam_train_steps_match_torch_adam(dev):
