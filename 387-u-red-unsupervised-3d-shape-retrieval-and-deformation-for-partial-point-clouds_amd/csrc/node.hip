@@ -29,12 +29,12 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 
 // Workgroup tile 32 x 32 (one MFMA tile), K split over the 8 waves in chunks of 32; the
 // independent GEMMs of one layer (e.g. a backward's dgrad and wgrad) share one launch as jobs.
-constexpr int NG_WAVES = 8, NG_NT = NG_WAVES * 64, NG_BM = 32, NG_BN = 32, NG_BK = 32, NG_JOBS = 4;
+constexpr int NG_WAVES = 8, NG_NT = NG_WAVES * 64, NG_BM = 32, NG_BN = 32, NG_BK = 32, NG_JOBS = URED_NODE_MAX_JOBS;
 
 struct NodeJob {
     UredNodeGemmDesc d;
     int akc, bkc;            // float4 fragment loads (k-contiguous, 16-B aligned operand)
-    int ntn;                 // column tiles
+    int ntn;                 // column tiles (kind 1: column blocks of 32)
 };
 struct NodeJobs {
     NodeJob job[NG_JOBS];
@@ -125,6 +125,22 @@ __global__ __launch_bounds__(NG_NT) void node_gemm_kernel(const NodeJobs jobs) {
     const NodeJob& J = jobs.job[ji];
     const UredNodeGemmDesc& d = J.d;
     const int tile = blockIdx.x - jobs.tile0[ji];
+    if (d.kind == URED_NODE_COLSUM) {         // bias gradient: C[n] (+)= sum_m A(m, n)
+        __shared__ float part[16][33];
+        const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5, n = tile * 32 + cl;
+        float sacc = 0.f;
+        if (n < d.N)
+            for (int m = rl; m < d.M; m += 16) sacc += d.A[(long long)m * d.sam + (long long)n * d.sak];
+        part[rl][cl] = sacc;
+        __syncthreads();
+        if (rl == 0 && n < d.N) {
+            float v = 0.f;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v += part[q][cl];
+            d.C[n] = d.accumulate ? d.C[n] + v : v;
+        }
+        return;
+    }
     const int m0 = (tile / J.ntn) * NG_BM, n0 = (tile % J.ntn) * NG_BN;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63, h = lane >> 5, li = lane & 31;
     const bool akc = J.akc, bkc = J.bkc;
@@ -302,6 +318,14 @@ extern "C" {
 
 static int check_node_job(const UredNodeGemmDesc& d, NodeJob& J) {
     URED_REQUIRE(d.M >= 0 && d.N >= 0 && d.K >= 0, "ured_node_gemm: bad sizes %d x %d x %d", d.M, d.N, d.K);
+    if (d.kind == URED_NODE_COLSUM) {
+        URED_REQUIRE(d.A && d.C, "ured_node_gemm: colsum job needs A and C");
+        J.d = d;
+        J.akc = J.bkc = 0;
+        J.ntn = (d.N + 31) / 32;
+        return 0;
+    }
+    URED_REQUIRE(d.kind == URED_NODE_GEMM, "ured_node_gemm: unknown job kind %d", d.kind);
     URED_REQUIRE(d.C && d.B && (d.A || d.k1 <= 0) && (d.A2 || d.k1 >= d.K), "ured_node_gemm: null operand");
     URED_REQUIRE(!d.rowbias || d.rdiv > 0, "ured_node_gemm: rowbias needs rdiv > 0");
     URED_REQUIRE(d.k1 >= d.K || d.k1 % 16 == 0, "ured_node_gemm: the A2 split k1 = %d must be a multiple of 16", d.k1);
@@ -329,7 +353,7 @@ int ured_node_gemm_batch(const UredNodeGemmDesc* const* ds, int n, void* stream)
         const int rc = check_node_job(d, J);
         if (rc) return rc;
         jobs.tile0[jobs.njobs] = tiles;
-        tiles += ((d.M + NG_BM - 1) / NG_BM) * J.ntn;
+        tiles += d.kind == URED_NODE_COLSUM ? J.ntn : ((d.M + NG_BM - 1) / NG_BM) * J.ntn;
         ++jobs.njobs;
     }
     if (jobs.njobs == 0) return 0;

@@ -53,4 +53,8 @@ def compute_contrast_loss_loss(tgt_part_f, src_f, src_labels, differentiable_gat
     s_e = F.normalize(s, dim=-1, p=2)
     _, s_all = all_gather_batch([t_e, s_e], differentiable=differentiable_gather)
     scale = torch.full((), LOGIT_SCALE, device=t.device).exp()   # a fill kernel: graph-capturable (no H2D copy)
+    if t_e.is_cuda:
+        # logits t_e s_all^T on the node GEMM (csrc/node.hip): forward and both backward GEMMs
+        from ured_hip.node import node_linear
+        return F.cross_entropy(node_linear(scale * t_e, s_all), labels, ignore_index=-1)
     return F.cross_entropy(scale * t_e @ s_all.t(), labels, ignore_index=-1)

@@ -37,7 +37,8 @@ class NodeGemmDesc(ctypes.Structure):
                 ("rowbias", _P), ("ldrb", _LL), ("rdiv", _I),
                 ("relu_out", _I),
                 ("gate", _P), ("ldgate", _LL),
-                ("R", _P), ("ldR", _LL), ("R_ncols", _I)]
+                ("R", _P), ("ldR", _LL), ("R_ncols", _I),
+                ("kind", _I)]
 
 
 class NodeBNDesc(ctypes.Structure):
@@ -59,7 +60,8 @@ class NodeBNBwdDesc(ctypes.Structure):
                 ("dgamma", _P), ("dbeta", _P), ("accumulate", _I)]
 
 
-MAX_JOBS = 4
+MAX_JOBS = 6
+KIND_GEMM, KIND_COLSUM = 0, 1
 _lib.register({"ured_node_gemm": [ctypes.POINTER(NodeGemmDesc), _P],
                "ured_node_gemm_batch": [ctypes.POINTER(ctypes.POINTER(NodeGemmDesc)), _I, _P],
                "ured_node_bn_fwd": [ctypes.POINTER(NodeBNDesc), _P],
@@ -96,6 +98,16 @@ def node_gemm_desc(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, *, A2=None, sam2=0
     d.relu_out = int(bool(relu_out))
     d.gate, d.ldgate = addr(gate), int(ldgate)
     d.R, d.ldR, d.R_ncols = addr(R), int(ldR), int(N if R_ncols is None else R_ncols)
+    d.kind = KIND_GEMM
+    return d
+
+
+def colsum_desc(g, out, accumulate=False):
+    """out [N] (+)= column sums of g [M, N] (a bias gradient), as a job of a batched launch."""
+    ga, gs = _mat(g)
+    M, N = g.shape
+    d = node_gemm_desc(M, N, 0, ga, gs, 1, ga, 0, 0, out, 0, accumulate=accumulate)
+    d.kind = KIND_COLSUM
     return d
 
 
@@ -249,10 +261,11 @@ class NodeLinearFn(Function):
         if ctx.needs_input_grad[1]:
             dW = torch.empty(W.shape, device=W.device)
             jobs.append(wgrad_desc(g, x, dW))
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.empty(g.shape[1], device=g.device)
+            jobs.append(colsum_desc(g, db))
         if jobs:
             launch(*jobs)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            db = colsum(g)
         return dx, dW, db, (g if ctx.has_r else None)
 
 
@@ -279,8 +292,10 @@ class NodeLinear2Fn(Function):
         g1, g2 = g1.contiguous(), g2.contiguous()
         dx1, dW1 = torch.empty(x1.shape, device=x1.device), torch.empty(W1.shape, device=W1.device)
         dx2, dW2 = torch.empty(x2.shape, device=x2.device), torch.empty(W2.shape, device=W2.device)
-        launch(dgrad_desc(g1, W1, dx1), wgrad_desc(g1, x1, dW1), dgrad_desc(g2, W2, dx2), wgrad_desc(g2, x2, dW2))
-        return dx1, dW1, colsum(g1), dx2, dW2, colsum(g2)
+        db1, db2 = torch.empty(g1.shape[1], device=g1.device), torch.empty(g2.shape[1], device=g2.device)
+        launch(dgrad_desc(g1, W1, dx1), wgrad_desc(g1, x1, dW1), dgrad_desc(g2, W2, dx2), wgrad_desc(g2, x2, dW2),
+               colsum_desc(g1, db1), colsum_desc(g2, db2))
+        return dx1, dW1, db1, dx2, dW2, db2
 
 
 def node_linear2(x1, W1, b1, x2, W2, b2):
@@ -323,13 +338,14 @@ class NodeFFNFn(Function):
         dev = x.device
         dact = torch.empty(act.shape, device=dev)
         dW2 = torch.empty(W2.shape, device=dev)
-        launch(dgrad_desc(g, W2, dact), wgrad_desc(g, act, dW2))
-        db2 = colsum(g)
+        db2 = torch.empty(W2.shape[0], device=dev)
+        launch(dgrad_desc(g, W2, dact), wgrad_desc(g, act, dW2), colsum_desc(g, db2))
         dY1, dgamma, dbeta = bn_bwd(dact, Y1, gamma, mean, invstd, off, training)
         dW1 = torch.empty(W1.shape, device=dev)
+        db1 = torch.empty(W1.shape[0], device=dev)
         dxm = torch.empty(M, 2 * C, device=dev)           # [d first | d message] in one GEMM
-        launch(wgrad_desc(dY1, x, dW1, x2=msg), dgrad_desc(dY1, W1, dxm, R=g if ctx.res_is_x else None, R_ncols=C))
-        db1 = colsum(dY1)
+        launch(wgrad_desc(dY1, x, dW1, x2=msg), dgrad_desc(dY1, W1, dxm, R=g if ctx.res_is_x else None, R_ncols=C),
+               colsum_desc(dY1, db1))
         return None, dxm[:, :C], dxm[:, C:], (None if ctx.res_is_x else g), dW1, db1, dgamma, dbeta, dW2, db2
 
 
@@ -369,16 +385,16 @@ class ParamDecoderFn(Function):
         g = g.contiguous()
         dev = g.device
         dW2 = torch.empty(W2.shape, device=dev)
+        db2 = torch.empty(W2.shape[0], device=dev)
         dh = torch.empty(h.shape, device=dev)
-        launch(wgrad_desc(g, h, dW2), dgrad_desc(g, W2, dh, gate=h))    # dh through the ReLU (h > 0)
-        db2 = colsum(g)
+        launch(wgrad_desc(g, h, dW2), dgrad_desc(g, W2, dh, gate=h), colsum_desc(g, db2))   # dh through the ReLU
         S = K.group_colsum(dh, dh.shape[1], B, group_rows=P)  # per-sample sums of the broadcast half
         dW1 = torch.empty(W1.shape, device=dev)
+        db1 = torch.empty(W1.shape[0], device=dev)
         dparts = torch.empty(parts.shape, device=dev)
         dglob = torch.empty(glob.shape, device=dev)
         launch(wgrad_desc(S, glob, dW1[:, :Cg]), wgrad_desc(dh, parts, dW1[:, Cg:]),
-               dgrad_desc(dh, W1[:, Cg:], dparts), dgrad_desc(S, W1[:, :Cg], dglob))
-        db1 = colsum(dh)
+               dgrad_desc(dh, W1[:, Cg:], dparts), dgrad_desc(S, W1[:, :Cg], dglob), colsum_desc(dh, db1))
         return None, dglob, dparts, dW1, db1, dW2, db2
 
 

@@ -35,6 +35,9 @@ import torch.distributed as dist  # noqa: E402
 PEAK_FP32_TFLOPS = 157.3      # MI355X fp32 (vector = matrix) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 PMC_SUMMARY = "r1g_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
+# rocprofv3 --kernel-trace --stats of the headline command (tools/prof_step.sh), restricted to its timed
+# steps: the dominant kernel's average duration there is what roofline.achieved / frac are computed from
+PROF_STATS = "r2_step_kernel_stats.csv"
 CLOCK_SUMMARY = "r1z_clock_summary.json"   # GRBM_GUI_ACTIVE pass (tools/gpu41.sh): clock held per kernel
 SQ_SUMMARY = "r1z_sq_summary.json"         # SQ pass (tools/gpu42.sh): MFMA-busy cycles per kernel
 NOMINAL_GHZ = 2.4
@@ -573,6 +576,23 @@ def main():
         avg_ms = d["ms"] / d["launches"]
         flop_per_launch = d["flop"] / d["launches"]
         ach = flop_per_launch / (avg_ms * 1e-3) / 1e12
+        live = {"avg_launch_ms": round(avg_ms, 4), "achieved": round(ach, 2),
+                "frac": round(ach / PEAK_FP32_TFLOPS, 4), "timing": timing}
+        # primary figures: the committed rocprof kernel-trace average of this kernel (same command,
+        # timed steps); the profiler lengthens in-step kernels by a few %, so the live
+        # HIP-event figures are reported beside them
+        prof = os.path.join(ROOT, "profiles", PROF_STATS)
+        prof_avg = None
+        if os.path.exists(prof):
+            import csv
+            with open(prof) as f:
+                for row in csv.DictReader(f):
+                    if dom_key in row["Name"]:
+                        prof_avg = float(row["AverageNs"]) * 1e-6
+        if prof_avg:
+            avg_ms, ach = prof_avg, flop_per_launch / (prof_avg * 1e-3) / 1e12
+            timing = (f"rocprofv3 kernel-trace average of this kernel over the timed steps of the same command "
+                      f"({os.path.relpath(prof, ROOT)})")
         traffic, tsrc = None, None
         pmc = os.path.join(ROOT, "profiles", PMC_SUMMARY)
         if os.path.exists(pmc):
@@ -585,7 +605,7 @@ def main():
                     "traffic": None if traffic is None else round(traffic), "traffic_source": tsrc,
                     "algorithmic_bytes_per_launch": round(d["bytes"] / d["launches"]),
                     "kernel": dom_key, "launches_per_step": round(lps, 2), "avg_launch_ms": round(avg_ms, 4),
-                    "flop_per_launch": round(flop_per_launch), "timing": timing}
+                    "flop_per_launch": round(flop_per_launch), "timing": timing, "live_hip_events": live}
         clk = os.path.join(ROOT, "profiles", CLOCK_SUMMARY)
         if os.path.exists(clk):
             for kname, v in json.load(open(clk)).items():

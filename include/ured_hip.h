@@ -323,7 +323,11 @@ int ured_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float*
  *   gate: v = gate[m*ldgate+n] > 0 ? v : 0; v += R[m*ldR+n] for n < R_ncols;
  *   accumulate: C += v, else C = v.
  * k1 >= K or k1 % 16 == 0. Nullable: A2, B2, bias, rowbias, gate, R. Deterministic (fixed split
- * and summation order). */
+ * and summation order).
+ * kind URED_NODE_COLSUM (a bias gradient riding in the same batched launch): C[n] (+)= sum over
+ * m < M of A[m*sam + n*sak], n < N (B, K unused). */
+#define URED_NODE_GEMM 0
+#define URED_NODE_COLSUM 1
 typedef struct {
     int M, N, K;
     const float* A; long long sam, sak;
@@ -336,10 +340,11 @@ typedef struct {
     int relu_out;
     const float* gate; long long ldgate;
     const float* R; long long ldR; int R_ncols;
+    int kind;
 } UredNodeGemmDesc;
 int ured_node_gemm(const UredNodeGemmDesc* d, void* stream);
 /* Up to URED_NODE_MAX_JOBS independent node GEMMs in one launch (no ordering between them). */
-#define URED_NODE_MAX_JOBS 4
+#define URED_NODE_MAX_JOBS 6
 int ured_node_gemm_batch(const UredNodeGemmDesc* const* d, int n, void* stream);
 
 /* BatchNorm1d over node sets: rows [off[s], off[s+1]) are one call of the module (the two node
