@@ -673,6 +673,9 @@ constexpr int PRO_LDS = 1024;            // max prologue channels staged in LDS 
 // SGPR spills (every epilogue argument stays live across the main loop), so it is compiled
 // out; kept for experiments.
 constexpr bool GEMM_PERSIST = false;
+#ifndef URED_DMA_SPREAD
+#define URED_DMA_SPREAD 1
+#endif
 #ifndef URED_PRO_PACKED
 #define URED_PRO_PACKED 0
 #endif
@@ -755,7 +758,11 @@ __device__ __forceinline__ void dma4(const i32x4& rsrc, unsigned v0, unsigned v1
 // lds: wave-uniform LDS byte address of this wave's first chunk of the operand image
 template <bool KM>
 __device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, unsigned lds) {
+#ifdef URED_DMA_FIXED   // timing experiment only: every K-step re-reads the first K-tile (wrong results)
+    const unsigned toff = 0u * (unsigned)k0 * (unsigned)ld;
+#else
     const unsigned toff = KM ? (unsigned)k0 * (unsigned)ld * 4u : (unsigned)k0 * 4u;
+#endif
     dma4(o.rsrc, o.vo[0] + toff, o.vo[1] + toff, o.vo[2] + toff, o.vo[3] + toff, lds);
 }
 
@@ -817,13 +824,15 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     // this wave's chunk base in the LDS images, as a wave-uniform byte address (SGPR)
     const unsigned lds_w = __builtin_amdgcn_readfirstlane(
         (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem + (unsigned)w * 4096u);
-    auto issue = [&](int stage, int k0, int m0_, int n0_) {
+    auto issue_a = [&](int stage, int k0) {
         const unsigned la = lds_w + (unsigned)stage * (2u * TILE * 4u);
-        const unsigned lb = la + TILE * 4u;
         if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false>(ba2, d.lda2, k0 - d.k1, la);
         else buf_tile<A_KM>(ba, d.lda, k0, la);
-        buf_tile<B_KM>(bb, d.ldb, k0, lb);
     };
+    auto issue_b = [&](int stage, int k0) {
+        buf_tile<B_KM>(bb, d.ldb, k0, lds_w + (unsigned)stage * (2u * TILE * 4u) + TILE * 4u);
+    };
+    auto issue = [&](int stage, int k0, int, int) { issue_a(stage, k0); issue_b(stage, k0); };
 
     if constexpr (PRO_IN_LDS) {   // visible after the first loop barrier
         for (int i = t; i < d.k1; i += NT) { pro_lds[i] = d.pro_s[i]; pro_lds[PRO_LDS + i] = d.pro_t[i]; }
@@ -868,9 +877,13 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             const float* As = smem + stage * 2 * TILE;
             const float* Bs = As + TILE;
             const bool tail = k0 + BK > kend;
-            // next step's DMA first (into the other stage: its last readers passed the barrier
-            // above); it lands while this step is read and multiplied
-            if (k0 + BK < kend) issue(stage ^ 1, k0 + BK, m0, n0);
+            // next step's DMA goes into the other stage (its last readers passed the barrier
+            // above). URED_DMA_SPREAD: its two 4-piece halves are issued between MFMA groups
+            // instead of in one burst in front of the fragment reads (an LDS-DMA piece costs its
+            // wave ~60 cycles among MFMAs, 100-185 beside the step's ds_reads; measured on the
+            // bare loop: 139 -> 146 TF/s, tools/mfma_clock.hip)
+            const bool next = k0 + BK < kend;
+            if (!URED_DMA_SPREAD && next) issue(stage ^ 1, k0 + BK, m0, n0);
 
             // the prologue's scale/shift first: LDS reads complete in issue order, so the
             // prologue (and the MFMAs behind it) can start on the first A fragments
@@ -965,6 +978,8 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                 acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[1][j], acc[0][1], 0, 0, 0);
                 acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[0][j], acc[1][0], 0, 0, 0);
                 acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][j], acc[1][1], 0, 0, 0);
+                if (URED_DMA_SPREAD && next && j == 1) issue_a(stage ^ 1, k0 + BK);
+                if (URED_DMA_SPREAD && next && j == 5) issue_b(stage ^ 1, k0 + BK);
             }
             stage ^= 1;
         }

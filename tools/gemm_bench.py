@@ -24,6 +24,13 @@ SHAPES = [  # (name, M, N, K)  — source encoder (M = 16*16*1024 points)
     ("src.mlp2.6 128->1024", 262144, 1024, 128),
     ("recon_src R1 512->256", 262144, 256, 512),
 ]
+STEP_SHAPES = [  # config-2 step sizes (unique-source encoding: M = 32768 target points, ~62-64 k source points)
+    ("step src.fuse 1024->1024", 62464, 1024, 1024),
+    ("step src.ppo0 1024->512", 62464, 512, 1024),
+    ("step tgt.ppo3 512->512", 32768, 512, 512),
+    ("step tgt.mlp 128->1024", 32768, 1024, 128),
+    ("step R1 512->256", 32768, 256, 512),
+]
 
 
 def timeit(fn, iters):
@@ -42,12 +49,13 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--step", action="store_true", help="the config-2 step's layer sizes instead of M=262144")
     a = ap.parse_args()
     ge.build()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     out = {}
-    for name, M, N, Kd in SHAPES:
+    for name, M, N, Kd in (STEP_SHAPES if a.step else SHAPES):
         X = torch.randn(M, Kd, device=dev, generator=g)
         W = torch.randn(N, Kd, device=dev, generator=g) * 0.05
         s = torch.rand(Kd, device=dev, generator=g) + 0.5
