@@ -6,5 +6,7 @@
   mlp      PointEncoderFn / ResidualNetFn autograd chains
   attn     graph-node multi-head attention (DeformNet's GraphAttentionNet core)
   optim    FlatAdam: per-module gradient clipping + Adam over flat buffers
+  node     DeformNet graph-node GEMM / BatchNorm launches
+  ops      device-side part building (segment sums, AABBs)
 """
-from . import _lib, attn, kernels, nn, optim  # noqa: F401
+from . import _lib, attn, kernels, nn, node, ops, optim  # noqa: F401
