@@ -341,20 +341,34 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
             const bool cv = col < d.N;
             const float bsv = bsv_[j];
+            if (!d.rowbias || rb_blk) {   // common case: no per-element branch or load
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = row_of(i, r);
+                        const float v = acc[i][j][r] + bsv;
+                        Cw.put(cv && row < d.M, row, col, v);
+                        acc[i][j][r] = v;
+                    }
+            } else {
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = row_of(i, r);
                     float v = acc[i][j][r] + bsv;
-                    if (d.rowbias && !rb_blk && cv && row < d.M) {
+                    if (cv && row < d.M) {
                         const int g = d.gidx ? d.gidx[row] : row / d.group_rows;
                         v += d.rowbias[(size_t)g * d.ldr + col];
                     }
                     Cw.put(cv && row < d.M, row, col, v);
                     acc[i][j][r] = v;
                 }
+            }
         }
+        // the statistics are of relu(v) (stat_relu) or v: a clamp at 0 or at -inf
+        const float plo = d.stat_relu ? 0.f : -__builtin_inff();
         // pass 1: column sums of p over valid rows
         float csum[2];
 #pragma unroll
@@ -364,7 +378,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const float p = d.stat_relu ? fmaxf(acc[i][j][r], 0.f) : acc[i][j][r];
+                    const float p = fmaxf(acc[i][j][r], plo);
                     s += (row_of(i, r) < d.M) ? p : 0.f;
                 }
             s += __shfl_xor(s, 32);
@@ -390,7 +404,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const float p = d.stat_relu ? fmaxf(acc[i][j][r], 0.f) : acc[i][j][r];
+                    const float p = fmaxf(acc[i][j][r], plo);
                     const float e = p - cmean[j];
                     s += (row_of(i, r) < d.M) ? e * e : 0.f;
                 }
@@ -500,6 +514,11 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         if (URED_BNBWD_YALL) { load_y(0); load_y(1); }   // behind the (L2-resident) per-column parameters
         pre();
         OutTile<BUFST> Gw(d.C, d.ldc, d.M, d.N);
+        // per-element global reads (a residual gradient, or pooled gradients of groups that do
+        // not align with the 128-row block) take the general loop below
+        const bool slow = d.gadd || (d.pool_idx && !pool_blk);
+        const bool relu_mask = d.bwd_res != URED_ACT_RES && d.bwd_res != URED_ACT_BN;
+        const float ylo = d.bwd_res == URED_ACT_RES ? 0.f : -__builtin_inff();
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (!URED_BNBWD_YALL && j == 1) load_y(1);
@@ -509,6 +528,27 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             const int pidx = pidx_[j];
             const float pgr = pgr_[j];
             float a1 = 0.f, a2 = 0.f;
+            if (!slow) {
+                // common case, branch-free per element: the activation mode as a clamp and a mask
+                // (ReLU mode: keep where y*sc+sh > 0; otherwise 0*y+1 > 0 keeps every element) and
+                // the block's pooled gradient as a select (pidx = -1 matches no row)
+                const float sck = relu_mask ? sc : 0.f, shk = relu_mask ? sh : 1.f;
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = row_of(i, r);
+                        const bool ok = cv && row < d.M;
+                        const float a = acc[i][j][r];
+                        const float dh = (row == pidx) ? a + pgr : a;
+                        const float y = yh[URED_BNBWD_YALL ? j : 0][i][r];
+                        const float xh = (fmaxf(y, ylo) - mu) * is;
+                        const float g = (__builtin_fmaf(y, sck, shk) > 0.f) ? dh : 0.f;
+                        Gw.put(ok, row, col, g);
+                        a1 += ok ? g : 0.f;
+                        a2 += ok ? g * xh : 0.f;
+                    }
+            } else {
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -539,6 +579,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                     a1 += ok ? g : 0.f;
                     a2 += ok ? g * xh : 0.f;
                 }
+            }
             a1 += __shfl_xor(a1, 32);
             a2 += __shfl_xor(a2, 32);
             s1[j] = a1; s2[j] = a2;

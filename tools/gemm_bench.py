@@ -50,6 +50,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--step", action="store_true", help="the config-2 step's layer sizes instead of M=262144")
+    ap.add_argument("--dgrad-layouts", action="store_true",
+                    help="also time store-only dgrad with the weight k-major vs pre-transposed (row-major)")
     a = ap.parse_args()
     ge.build()
     dev = torch.device("cuda:0")
@@ -78,6 +80,10 @@ def main():
                                          a.iters) / 1e12
         r["dgrad_bnbwd"] = flop / timeit(lambda: K.gemm(M, Kd, N, dY, N, W, Kd, G, Kd, b_kmajor=True, epi=K.EPI_BNBWD,
                                                         Yp=X, ldy=Kd, bn=st, bwd_ws=bws), a.iters) / 1e12
+        if a.dgrad_layouts:
+            Wt = W.t().contiguous()   # [Kd][N]: the dgrad B operand row-major (k = N contiguous)
+            r["dgrad_store"] = flop / timeit(lambda: K.gemm(M, Kd, N, dY, N, W, Kd, G, Kd, b_kmajor=True), a.iters) / 1e12
+            r["dgrad_store_T"] = flop / timeit(lambda: K.gemm(M, Kd, N, dY, N, Wt, N, G, Kd), a.iters) / 1e12
         r["wgrad"] = flop / timeit(lambda: K.wgrad(dY, N, X, Kd, N, Kd, M, dW, Kd, pro=K.PRO_ENC, pro_s=s, pro_t=t),
                                    a.iters) / 1e12
         out[name] = {k: round(v, 1) for k, v in r.items()}
