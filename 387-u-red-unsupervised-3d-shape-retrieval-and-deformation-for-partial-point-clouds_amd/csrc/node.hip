@@ -129,8 +129,12 @@ __global__ __launch_bounds__(NG_NT) void node_gemm_kernel(const NodeJobs jobs) {
         __shared__ float part[16][33];
         const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5, n = tile * 32 + cl;
         float sacc = 0.f;
-        if (n < d.N)
-            for (int m = rl; m < d.M; m += 16) sacc += d.A[(long long)m * d.sam + (long long)n * d.sak];
+        if (n < d.N) {
+            // unrolled so that eight loads are in flight per lane (the adds keep their order)
+            const float* col = d.A + (long long)n * d.sak;
+#pragma unroll 8
+            for (int m = rl; m < d.M; m += 16) sacc += col[(long long)m * d.sam];
+        }
         part[rl][cl] = sacc;
         __syncthreads();
         if (rl == 0 && n < d.N) {

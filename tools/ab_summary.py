@@ -1,4 +1,5 @@
-"""Summarise an A/B log of tools/ab_lib_gemm.sh: per shape and variant, the A and B rates of each run.
+"""Summarise an A/B log of tools/ab_lib_gemm.sh: per shape and variant, the rates of each library
+(A = in-tree, B, C, ... = the URED_LIB builds) and each one's ratio to A.
   python tools/ab_summary.py gpurun_out/ab.log [variant ...]"""
 import ast
 import collections
@@ -19,7 +20,14 @@ keys = sys.argv[2:]
 for shape, dd in R.items():
     ks = keys or sorted({k for _, k in dd})
     print(shape)
+    tags = sorted({t for t, _ in dd})
     for k in ks:
-        a, b = dd[("A", k)], dd[("B", k)]
-        if a and b:
-            print(f"   {k:14s} A {a}  B {b}  A/B {sum(a) / sum(b):.3f}")
+        a = dd[("A", k)]
+        if not a:
+            continue
+        row = f"   {k:14s} A {a}"
+        for t in tags[1:]:
+            b = dd[(t, k)]
+            if b:
+                row += f"  {t} {b} {t}/A {sum(b) / sum(a):.3f}"
+        print(row)
