@@ -3,7 +3,8 @@
 Module/attribute names match the reference so checkpoints interchange. The graph has
 2 global + MAX_NUM_PARTS part nodes per sample: tiny, launch-bound work. The U-RED step
 runs it node-major (`forward_nodes`, [B, nodes, C]) on HIP kernels only: the q|k|v
-projections as one node GEMM (ured_hip.node, csrc/node.hip), the attention core as one
+projections as one node GEMM over the parameters' own back-to-back memory (ured_hip.node
+NodeProjFn, csrc/node.hip), the attention core as one
 kernel each way (ured_hip.attn), out_proj as a node GEMM, and the FeedForwardNet_norm update
 (conv -> ReLU -> BatchNorm per node set -> conv, + residual) as two node GEMMs around one
 BatchNorm kernel, the concatenation [x, message] read in place. `forward` keeps the
@@ -13,7 +14,7 @@ import torch
 import torch.nn as nn
 
 from ured_hip.attn import cross_attention, self_attention
-from ured_hip.node import node_ffn, node_linear, node_linear2
+from ured_hip.node import node_ffn, node_linear, node_proj
 
 from . import get_attention_mechanism
 from .attention import softmax_attention
@@ -30,6 +31,12 @@ class MultiheadAttention(nn.Module):
         self.in_proj_k = nn.Conv1d(embed_dim, embed_dim, kernel_size=1)
         self.in_proj_v = nn.Conv1d(embed_dim, embed_dim, kernel_size=1)
         self.out_proj = nn.Conv1d(embed_dim, embed_dim, kernel_size=1)
+        # FlatAdam lays these chains out back to back, so the node layers read q|k|v (and k|v) as
+        # one matrix / bias vector without concatenating them (ured_hip.node.NodeProjFn)
+        for name in ("weight", "bias"):
+            chain = tuple(getattr(c, name) for c in (self.in_proj_q, self.in_proj_k, self.in_proj_v))
+            for prm in chain:
+                prm._ured_chain = chain
 
     def forward(self, query, key, value):
         b = query.shape[0]
@@ -51,13 +58,13 @@ class MultiheadAttention(nn.Module):
         q_, k_, v_ = self.in_proj_q, self.in_proj_k, self.in_proj_v
         B, n, C = xq.shape
         if xkv is None:
-            qkv = node_linear(xq.reshape(B * n, C), torch.cat([self._w(q_), self._w(k_), self._w(v_)]),
-                              torch.cat([q_.bias, k_.bias, v_.bias]))
+            qkv = node_proj((xq.reshape(B * n, C),), [(self._w(q_), self._w(k_), self._w(v_))],
+                            [(q_.bias, k_.bias, v_.bias)])
             out = self_attention(qkv.view(B, n, 3 * C), self.num_heads)
         else:
             m = xkv.shape[1]
-            q, kv = node_linear2(xq.reshape(B * n, C), self._w(q_), q_.bias,
-                                 xkv.reshape(B * m, C), torch.cat([self._w(k_), self._w(v_)]), torch.cat([k_.bias, v_.bias]))
+            q, kv = node_proj((xq.reshape(B * n, C), xkv.reshape(B * m, C)),
+                              [(self._w(q_),), (self._w(k_), self._w(v_))], [(q_.bias,), (k_.bias, v_.bias)])
             out = cross_attention(q.view(B, n, C), kv.view(B, m, 2 * C), self.num_heads)
         return node_linear(out.reshape(B * n, C), self._w(self.out_proj), self.out_proj.bias).view(B, n, C)
 
@@ -101,7 +108,7 @@ class ResidualAttentionMessagePropagation(nn.Module):
         R0, R1 = B * n0, B * n1
         X = torch.cat([x0.reshape(R0, C), x1.reshape(R1, C)])
         q_, k_, v_ = mha.in_proj_q, mha.in_proj_k, mha.in_proj_v
-        qkv = node_linear(X, torch.cat([mha._w(q_), mha._w(k_), mha._w(v_)]), torch.cat([q_.bias, k_.bias, v_.bias]))
+        qkv = node_proj((X,), [(mha._w(q_), mha._w(k_), mha._w(v_))], [(q_.bias, k_.bias, v_.bias)])
         q0, q1 = qkv.split([R0, R1])          # split (backward: one cat) rather than slices
         o = torch.cat([self_attention(q0.view(B, n0, -1), mha.num_heads).reshape(R0, C),
                        self_attention(q1.view(B, n1, -1), mha.num_heads).reshape(R1, C)])

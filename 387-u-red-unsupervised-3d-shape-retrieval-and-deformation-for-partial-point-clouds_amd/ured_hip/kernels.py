@@ -209,10 +209,11 @@ def group_colsum(X, N, G, *, off=None, group_rows=0, ldx=None, out=None, rows=No
     return out
 
 
-def colsum(X):
-    """Column sums of a [R][N] tensor (deterministic: fixed split ranges and combine order)."""
+def colsum(X, out=None):
+    """Column sums of a [R][N] tensor (deterministic: fixed split ranges and combine order);
+    into `out` [N] (contiguous) when given."""
     R, N = X.shape
-    return group_colsum(X, N, 1, group_rows=R)[0]
+    return group_colsum(X, N, 1, group_rows=R, out=None if out is None else out.view(1, N))[0]
 
 
 SKINNY_WS_BLOCKS = 256          # URED_SKINNY_WS_BLOCKS (include/ured_hip.h)

@@ -18,6 +18,7 @@ from torch.autograd import Function
 
 from . import _lib
 from . import kernels as K
+from .optim import grad_buffer
 
 BN_EPS = 1e-5
 
@@ -143,14 +144,14 @@ class PointEncoderFn(Function):
         NP = pooled.shape[1]
         dpool = torch.empty(G, NP, device=dev)
         K.gemm(G, NP, C, dcode, C, fcW, NP, dpool, NP, b_kmajor=True)
-        dfcW = torch.empty_like(fcW)
+        dfcW = grad_buffer(fcW)
         K.wgrad(dcode, C, pooled, NP, C, NP, G, dfcW, NP)
-        grads[30], grads[31] = dfcW, K.colsum(dcode)
+        grads[30], grads[31] = dfcW, K.colsum(dcode, out=grad_buffer(params[31]))
         # per_point_out.3 (no BN): dW8 = dpp^T @ H7
-        dW8 = torch.empty(W8.shape, device=dev)
+        dW8 = grad_buffer(params[28]).view(W8.shape)
         K.wgrad(dpp, C, Ys[6], Ys[6].shape[1], C, W8.shape[1], M, dW8, W8.shape[1],
                 pro=K.PRO_ENC, pro_s=states[6].scale, pro_t=states[6].shift)
-        grads[28], grads[29] = dW8.view(params[28].shape), K.colsum(dpp)
+        grads[28], grads[29] = dW8.view(params[28].shape), K.colsum(dpp, out=grad_buffer(params[29]))
         dY, Wn = dpp, W8   # gradient at the output of the layer above, and that layer's weight
         for i in range(6, -1, -1):
             Y, st = Ys[i], states[i]
@@ -164,11 +165,11 @@ class PointEncoderFn(Function):
             # dH_i = dY_{i+1} @ W_{i+1}[:, :N]; fused ReLU mask + BN-backward partials of layer i
             K.gemm(M, N, Cn, dY, Cn, Wn, Wn.shape[1], G_, N, b_kmajor=True, epi=K.EPI_BNBWD,
                    Yp=Y, ldy=N, bn=st, bwd_res=False, bwd_ws=bws, **kw)
-            dgamma, dbeta = torch.empty(N, device=dev), torch.empty(N, device=dev)
+            dgamma, dbeta = grad_buffer(gs[i]), grad_buffer(params[4 * i + 3])
             coefs = K.bn_bwd_finalize(bws, M, N, gs[i], st.invstd, dgamma, dbeta, rw=spec.rw)
             dYi, cs = K.bn_bwd_apply(G_, Y, False, st.mean, coefs, rw=spec.rw)
             W = Ws[i]
-            dW = torch.empty(W.shape, device=dev)
+            dW = grad_buffer(params[4 * i]).view(W.shape)
             if i == 0:
                 K.wgrad(dYi, N, x, 3, N, 3, M, dW, 3)
             else:
@@ -183,7 +184,7 @@ class PointEncoderFn(Function):
                     else:
                         K.wgrad(dYi, N, sem, S, N, S, M, dW, W.shape[1], out_off=kin)
             grads[4 * i] = dW.view(params[4 * i].shape)
-            grads[4 * i + 1] = K.colsum(cs)
+            grads[4 * i + 1] = K.colsum(cs, out=grad_buffer(params[4 * i + 1]))
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
         return (None, None, None) + tuple(grads)
@@ -272,10 +273,10 @@ class ResidualNetFn(Function):
         dout = dout.contiguous()
         W4 = params[12].reshape(params[12].shape[0], -1)
         No = W4.shape[0]
-        dW4 = torch.empty(W4.shape, device=dev)
+        dW4 = grad_buffer(params[12]).view(W4.shape)
         K.wgrad(dout, No, Ys[2], Ys[2].shape[1], No, W4.shape[1], M, dW4, W4.shape[1],
                 pro=K.PRO_RES, pro_s=states[2].scale, pro_t=states[2].shift)
-        grads[12], grads[13] = dW4.view(params[12].shape), K.colsum(dout)
+        grads[12], grads[13] = dW4.view(params[12].shape), K.colsum(dout, out=grad_buffer(params[13]))
         dY, Wn = dout, W4
         W1 = params[0].reshape(params[0].shape[0], -1)
         ld1 = W1.shape[1]
@@ -288,11 +289,11 @@ class ResidualNetFn(Function):
             bws = torch.empty(K.nblocks(M), 2, N, device=dev)
             K.gemm(M, N, Cn, dY, Cn, Wn, Wn.shape[1], G_, N, b_kmajor=True, epi=K.EPI_BNBWD,
                    Yp=Y, ldy=N, bn=st, bwd_res=True, bwd_ws=bws)
-            dgamma, dbeta = torch.empty(N, device=dev), torch.empty(N, device=dev)
+            dgamma, dbeta = grad_buffer(params[4 * i + 2]), grad_buffer(params[4 * i + 3])
             coefs = K.bn_bwd_finalize(bws, M, N, params[4 * i + 2], st.invstd, dgamma, dbeta, rw=rw)
             dYi, cs = K.bn_bwd_apply(G_, Y, True, st.mean, coefs, rw=rw)
             W = params[4 * i].reshape(params[4 * i].shape[0], -1)
-            dW = torch.empty(W.shape, device=dev)
+            dW = grad_buffer(params[4 * i]).view(W.shape)
             if i == 0:
                 K.wgrad(dYi, N, pp, Cp, N, Cp, M, dW, ld1, out_off=pp_off)
                 D = None
@@ -307,7 +308,7 @@ class ResidualNetFn(Function):
                 K.wgrad(dYi, N, Xp, Xp.shape[1], N, Xp.shape[1], M, dW, W.shape[1],
                         pro=K.PRO_RES, pro_s=stp.scale, pro_t=stp.shift)
             grads[4 * i] = dW.view(params[4 * i].shape)
-            grads[4 * i + 1] = K.colsum(cs)
+            grads[4 * i + 1] = K.colsum(cs, out=grad_buffer(params[4 * i + 1]))
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
         # input gradients: dpp = dY1 @ W1[:, pp cols]; dcode = D @ W1[:, code cols]
@@ -431,11 +432,11 @@ class PointChainFn(Function):
                 K.gemm(M, N, Cn, dY, Cn, Wn, Wn.shape[1], G_, N, b_kmajor=True, epi=K.EPI_BNBWD,
                        Yp=Y, ldy=N, bn=st, bwd_res=spec.acts[i], bwd_ws=bws)
             gamma = params[4 * i + 2]
-            dgamma, dbeta = torch.empty(N, device=dev), torch.empty(N, device=dev)
+            dgamma, dbeta = grad_buffer(gamma), grad_buffer(params[4 * i + 3])
             coefs = K.bn_bwd_finalize(bws, M, N, gamma, st.invstd, dgamma, dbeta)
             dYi, cs = K.bn_bwd_apply(G_, Y, False, st.mean, coefs)
             W = params[4 * i].reshape(params[4 * i].shape[0], -1)
-            dW = torch.empty(W.shape, device=dev)
+            dW = grad_buffer(params[4 * i]).view(W.shape)
             if i == 0:
                 K.wgrad(dYi, N, x, Cin, N, Cin, M, dW, Cin)
             else:
@@ -443,7 +444,7 @@ class PointChainFn(Function):
                 kin = Xp.shape[1]
                 K.wgrad(dYi, N, Xp, kin, N, kin, M, dW, kin, pro=K.PRO_ENC, pro_s=stp.scale, pro_t=stp.shift)
             grads[4 * i] = dW.view(params[4 * i].shape)
-            grads[4 * i + 1] = K.colsum(cs)
+            grads[4 * i + 1] = K.colsum(cs, out=grad_buffer(params[4 * i + 1]))
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
         dx = None

@@ -2,8 +2,9 @@
 Functions over node-major [rows, C] tensors (rows = B x nodes).
 
 NodeLinearFn   one Conv1d(k=1) over nodes: y = x W^T + b (+ residual); forward and both
-               backward GEMMs on ured_node_gemm (in_proj_q / k / v fused, out_proj;
-               attention_graph/attention_gnn.py:20-32).
+               backward GEMMs on ured_node_gemm (out_proj; attention_graph/attention_gnn.py:20-32).
+NodeProjFn     row-stacked projections (in_proj q|k|v of a self-attention, q and k|v of a
+               cross-attention) over the parameters' own back-to-back memory (FlatAdam chains).
 NodeFFNFn      ResidualAttentionMessagePropagation's update (attention_gnn.py:50-54):
                out = x + conv2(BN(relu(conv1(cat([first, message]))))) with
                FeedForwardNet_norm [2C, 2C, C] (attention_utils.py:62-86); the concatenation is
@@ -11,6 +12,10 @@ NodeFFNFn      ResidualAttentionMessagePropagation's update (attention_gnn.py:50
 ParamDecoderFn param_decoder (network/deformation_net.py:61,90): Conv 3C->256 -> ReLU ->
                Conv 256->6 on cat([global pair broadcast to the parts, part nodes]); the global
                half is a per-sample row bias (never broadcast).
+Parameter gradients go straight into FlatAdam's flat gradient (ured_hip.optim.grad_slot):
+written by the first use of a parameter in a backward, accumulated in the kernels by a second
+use (the cross-attention module updates both node sets with the same weights), so autograd has
+no gradient to copy or add.
 Reference semantics: Conv1d over [B, C, nodes] == a linear map of each node row; BatchNorm1d
 on [B, C, n] == per-channel statistics over the B*n node rows of one call.
 """
@@ -21,6 +26,7 @@ from torch.autograd import Function
 
 from . import _lib
 from . import kernels as K
+from .optim import grad_buffer, grad_slot
 
 _P, _I, _LL, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float
 MAX_SETS = 4
@@ -214,12 +220,12 @@ def bn_fwd(Y, bnm, off, training, relu_in=True):
     return act, mean, invstd
 
 
-def bn_bwd(G, Y, gamma, mean, invstd, off, training, relu_in=True):
+def bn_bwd(G, Y, gamma, mean, invstd, off, training, relu_in=True, dgamma=None, dbeta=None, accumulate=False):
     R, N = Y.shape
     nsets, arr = _sets(off)
     dY = torch.empty_like(Y)
-    dgamma = torch.empty(N, device=Y.device)
-    dbeta = torch.empty(N, device=Y.device)
+    dgamma = torch.empty(N, device=Y.device) if dgamma is None else dgamma
+    dbeta = torch.empty(N, device=Y.device) if dbeta is None else dbeta
     d = NodeBNBwdDesc()
     d.N, d.nsets, d.off = N, nsets, arr
     d.G, d.ldg = G.data_ptr(), G.stride(0)
@@ -227,7 +233,7 @@ def bn_bwd(G, Y, gamma, mean, invstd, off, training, relu_in=True):
     d.relu_in, d.training = int(relu_in), int(bool(training))
     d.gamma, d.mean, d.invstd = gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr()
     d.dY, d.lddy = dY.data_ptr(), dY.stride(0)
-    d.dgamma, d.dbeta, d.accumulate = dgamma.data_ptr(), dbeta.data_ptr(), 0
+    d.dgamma, d.dbeta, d.accumulate = dgamma.data_ptr(), dbeta.data_ptr(), int(bool(accumulate))
     _lib.call("ured_node_bn_bwd", ctypes.byref(d), _lib.stream_of(Y))
     return dY, dgamma, dbeta
 
@@ -247,6 +253,7 @@ class NodeLinearFn(Function):
         linear(x, W, y, bias=b, R=R)
         ctx.save_for_backward(x, W)
         ctx.has_b, ctx.has_r = b is not None, R is not None
+        ctx.b = b if (b is not None and b.is_leaf) else None    # a parameter: grad_buffer target
         return y
 
     @staticmethod
@@ -258,48 +265,136 @@ class NodeLinearFn(Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty(x.shape, device=x.device)
             jobs.append(dgrad_desc(g, W, dx))
+        accW = accb = False
         if ctx.needs_input_grad[1]:
-            dW = torch.empty(W.shape, device=W.device)
-            jobs.append(wgrad_desc(g, x, dW))
+            dW, accW = grad_slot(W)
+            jobs.append(wgrad_desc(g, x, dW, accumulate=accW))
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = torch.empty(g.shape[1], device=g.device)
-            jobs.append(colsum_desc(g, db))
+            db, accb = grad_slot(ctx.b) if ctx.b is not None else (torch.empty(g.shape[1], device=g.device), False)
+            jobs.append(colsum_desc(g, db, accumulate=accb))
         if jobs:
             launch(*jobs)
-        return dx, dW, db, (g if ctx.has_r else None)
+        return dx, (None if accW else dW), (None if accb else db), (g if ctx.has_r else None)
 
 
 def node_linear(x, W, b=None, R=None):
     return NodeLinearFn.apply(x, W, b, R)
 
 
-class NodeLinear2Fn(Function):
-    """Two independent node linears (y1 = x1 W1^T + b1, y2 = x2 W2^T + b2) in one launch each
-    way: a cross-attention's q and k|v projections."""
+def fused_rows(ts):
+    """ONE [sum of rows, ...] view over tensors that lie back to back in memory (FlatAdam lays out
+    chained parameters that way: an attention's in_proj q/k/v weights and biases), else None."""
+    t0 = ts[0]
+    if not t0.is_contiguous():
+        return None
+    if len(ts) == 1:
+        return t0.detach()
+    end = t0.data_ptr() + t0.numel() * t0.element_size()
+    base = t0.untyped_storage().data_ptr()     # one allocation: separate tensors may abut by chance
+    for t in ts[1:]:
+        if (not t.is_contiguous() or t.shape[1:] != t0.shape[1:] or t.data_ptr() != end or t.dtype != t0.dtype
+                or t.untyped_storage().data_ptr() != base):
+            return None
+        end += t.numel() * t.element_size()
+    return t0.detach().as_strided((sum(t.shape[0] for t in ts),) + tuple(t0.shape[1:]), t0.stride())
+
+
+def _stack_rows(ts):
+    f = fused_rows(ts)
+    return f if f is not None else torch.cat([t.detach() for t in ts])
+
+
+def _grad_rows(ts):
+    """Gradient storage of row-stacked parameters `ts` for one kernel job:
+    (buffer [sum of rows, ...], accumulate, finish) where finish() returns the per-part gradients
+    to hand to autograd (None for a part accumulated in place, grad_slot)."""
+    slots = [grad_slot(t) for t in ts]
+    bufs, accs = [b for b, _ in slots], [a for _, a in slots]
+    if all(a == accs[0] for a in accs):
+        f = fused_rows(bufs)
+        if f is not None:                     # the flat views are adjacent: write them in place
+            return f, accs[0], lambda: [None if accs[0] else b for b in bufs]
+    buf = torch.empty((sum(t.shape[0] for t in ts),) + tuple(ts[0].shape[1:]), device=ts[0].device)
+
+    def finish():
+        out, o = [], 0
+        for b, acc, t in zip(bufs, accs, ts):
+            part = buf[o:o + t.shape[0]]
+            o += t.shape[0]
+            if b._base is None:               # a fresh tensor (no flat slot): hand over the slice
+                out.append(part)
+            else:                             # a claimed flat view must receive the gradient
+                (b.add_ if acc else b.copy_)(part)
+                out.append(None if acc else b)
+        return out
+    return buf, False, finish
+
+
+class NodeProjFn(Function):
+    """Row-stacked projections of node sets: for input i, y_i = x_i W_i^T + b_i where W_i / b_i
+    stack the weights / biases of group i along rows — the q|k|v projections of a self-attention
+    (one input), the q and the k|v projections of a cross-attention (two inputs). When FlatAdam
+    has laid the chained parameters out back to back (MultiheadAttention declares the chain) the
+    stack is the parameters' own memory: no concatenation forward, and the weight / bias
+    gradients are written (or, for a second use of the layer, accumulated) straight into the flat
+    gradient. All GEMMs of one direction run in one launch.
+
+    apply(groups, x_0, .., x_{n-1}, then per input: its weights, then its biases)."""
 
     @staticmethod
-    def forward(ctx, x1, W1, b1, x2, W2, b2):
-        _lib.require_device(x1, W1, x2, W2)
-        y1 = torch.empty(x1.shape[0], W1.shape[0], device=x1.device)
-        y2 = torch.empty(x2.shape[0], W2.shape[0], device=x2.device)
-        launch(linear_desc(x1, W1, y1, bias=b1), linear_desc(x2, W2, y2, bias=b2))
-        ctx.save_for_backward(x1, W1, x2, W2)
-        return y1, y2
+    def forward(ctx, groups, *tensors):
+        n = len(groups)
+        xs, rest = tensors[:n], tensors[n:]
+        _lib.require_device(*xs)
+        Ws, bs, o = [], [], 0
+        for gsz in groups:
+            Ws.append(rest[o:o + gsz])
+            bs.append(rest[o + gsz:o + 2 * gsz])
+            o += 2 * gsz
+        ys, jobs = [], []
+        for x, w, b in zip(xs, Ws, bs):
+            Wf, bf = _stack_rows(w), _stack_rows(b)
+            y = torch.empty(x.shape[0], Wf.shape[0], device=x.device)
+            jobs.append(linear_desc(x, Wf, y, bias=bf))
+            ys.append(y)
+        launch(*jobs)
+        ctx.groups = groups
+        ctx.save_for_backward(*xs, *rest)
+        return tuple(ys) if n > 1 else ys[0]
 
     @staticmethod
-    def backward(ctx, g1, g2):
-        x1, W1, x2, W2 = ctx.saved_tensors
-        g1, g2 = g1.contiguous(), g2.contiguous()
-        dx1, dW1 = torch.empty(x1.shape, device=x1.device), torch.empty(W1.shape, device=W1.device)
-        dx2, dW2 = torch.empty(x2.shape, device=x2.device), torch.empty(W2.shape, device=W2.device)
-        db1, db2 = torch.empty(g1.shape[1], device=g1.device), torch.empty(g2.shape[1], device=g2.device)
-        launch(dgrad_desc(g1, W1, dx1), wgrad_desc(g1, x1, dW1), dgrad_desc(g2, W2, dx2), wgrad_desc(g2, x2, dW2),
-               colsum_desc(g1, db1), colsum_desc(g2, db2))
-        return dx1, dW1, db1, dx2, dW2, db2
+    def backward(ctx, *gs):
+        groups = ctx.groups
+        n = len(groups)
+        saved = ctx.saved_tensors
+        xs, rest = saved[:n], saved[n:]
+        jobs, dxs, fins, o = [], [], [], 0
+        for i, gsz in enumerate(groups):
+            w, b = rest[o:o + gsz], rest[o + gsz:o + 2 * gsz]
+            o += 2 * gsz
+            g = gs[i].contiguous()
+            x = xs[i]
+            dx = torch.empty(x.shape, device=x.device)
+            dW, aW, fW = _grad_rows(w)
+            db, ab, fb = _grad_rows(b)
+            jobs += [dgrad_desc(g, _stack_rows(w), dx), wgrad_desc(g, x, dW, accumulate=aW),
+                     colsum_desc(g, db, accumulate=ab)]
+            dxs.append(dx)
+            fins.append((fW, fb))
+        launch(*jobs)
+        out = [None] + dxs
+        for fW, fb in fins:
+            out += fW() + fb()
+        return tuple(out)
 
 
-def node_linear2(x1, W1, b1, x2, W2, b2):
-    return NodeLinear2Fn.apply(x1, W1, b1, x2, W2, b2)
+def node_proj(xs, groups_w, groups_b):
+    """NodeProjFn over inputs xs with weight groups groups_w[i] (tuples of [N_j, K] tensors) and
+    bias groups groups_b[i]."""
+    args = list(xs)
+    for w, b in zip(groups_w, groups_b):
+        args += list(w) + list(b)
+    return NodeProjFn.apply(tuple(len(w) for w in groups_w), *args)
 
 
 class NodeFFNFn(Function):
@@ -326,6 +421,7 @@ class NodeFFNFn(Function):
         out = torch.empty(M, W2.shape[0], device=dev)
         linear(act, W2, out, bias=b2, R=R)
         ctx.spec = spec
+        ctx.bparams = (b1, beta, b2)
         ctx.save_for_backward(x, msg, W1, gamma, W2, Y1, act, mean, invstd)
         return out
 
@@ -336,17 +432,25 @@ class NodeFFNFn(Function):
         g = g.contiguous()
         M, C = x.shape
         dev = x.device
+        b1, beta, b2 = ctx.bparams
         dact = torch.empty(act.shape, device=dev)
-        dW2 = torch.empty(W2.shape, device=dev)
-        db2 = torch.empty(W2.shape[0], device=dev)
-        launch(dgrad_desc(g, W2, dact), wgrad_desc(g, act, dW2), colsum_desc(g, db2))
-        dY1, dgamma, dbeta = bn_bwd(dact, Y1, gamma, mean, invstd, off, training)
-        dW1 = torch.empty(W1.shape, device=dev)
-        db1 = torch.empty(W1.shape[0], device=dev)
+        (dW2, aW2), (db2, ab2) = grad_slot(W2), grad_slot(b2)
+        launch(dgrad_desc(g, W2, dact), wgrad_desc(g, act, dW2, accumulate=aW2), colsum_desc(g, db2, accumulate=ab2))
+        (dgamma, ag), (dbeta, abe) = grad_slot(gamma), grad_slot(beta)
+        if ag == abe:
+            dY1, dgamma, dbeta = bn_bwd(dact, Y1, gamma, mean, invstd, off, training, dgamma=dgamma, dbeta=dbeta,
+                                        accumulate=ag)
+        else:                  # the BN kernel accumulates both or neither: settle each one after it
+            dY1, tg, tb = bn_bwd(dact, Y1, gamma, mean, invstd, off, training)
+            for buf, acc, tmp in ((dgamma, ag, tg), (dbeta, abe, tb)):
+                (buf.add_ if acc else buf.copy_)(tmp)
+        (dW1, aW1), (db1, ab1) = grad_slot(W1), grad_slot(b1)
         dxm = torch.empty(M, 2 * C, device=dev)           # [d first | d message] in one GEMM
-        launch(wgrad_desc(dY1, x, dW1, x2=msg), dgrad_desc(dY1, W1, dxm, R=g if ctx.res_is_x else None, R_ncols=C),
-               colsum_desc(dY1, db1))
-        return None, dxm[:, :C], dxm[:, C:], (None if ctx.res_is_x else g), dW1, db1, dgamma, dbeta, dW2, db2
+        launch(wgrad_desc(dY1, x, dW1, accumulate=aW1, x2=msg),
+               dgrad_desc(dY1, W1, dxm, R=g if ctx.res_is_x else None, R_ncols=C), colsum_desc(dY1, db1, accumulate=ab1))
+        return (None, dxm[:, :C], dxm[:, C:], (None if ctx.res_is_x else g),
+                *(None if acc else t for t, acc in ((dW1, aW1), (db1, ab1), (dgamma, ag), (dbeta, abe), (dW2, aW2),
+                                                    (db2, ab2))))
 
 
 def node_ffn(fc, x, msg, R, off):
@@ -374,6 +478,7 @@ class ParamDecoderFn(Function):
         out = torch.empty(BP, W2.shape[0], device=dev)
         linear(h, W2, out, bias=b2)
         ctx.P = P
+        ctx.bparams = (b1, b2)
         ctx.save_for_backward(glob, parts, W1, W2, h)
         return out
 
@@ -384,13 +489,14 @@ class ParamDecoderFn(Function):
         B, Cg = glob.shape
         g = g.contiguous()
         dev = g.device
-        dW2 = torch.empty(W2.shape, device=dev)
-        db2 = torch.empty(W2.shape[0], device=dev)
+        b1, b2 = ctx.bparams
+        dW2 = grad_buffer(W2)
+        db2 = grad_buffer(b2)
         dh = torch.empty(h.shape, device=dev)
         launch(wgrad_desc(g, h, dW2), dgrad_desc(g, W2, dh, gate=h), colsum_desc(g, db2))   # dh through the ReLU
         S = K.group_colsum(dh, dh.shape[1], B, group_rows=P)  # per-sample sums of the broadcast half
-        dW1 = torch.empty(W1.shape, device=dev)
-        db1 = torch.empty(W1.shape[0], device=dev)
+        dW1 = grad_buffer(W1)
+        db1 = grad_buffer(b1)
         dparts = torch.empty(parts.shape, device=dev)
         dglob = torch.empty(glob.shape, device=dev)
         launch(wgrad_desc(S, glob, dW1[:, :Cg]), wgrad_desc(dh, parts, dW1[:, Cg:]),

@@ -33,6 +33,7 @@ scalar only when it changes (call sync_lr() before replaying a captured step aft
 change). optimizer.state holds the flat moments and the per-parameter step counts under "flat".
 """
 import ctypes
+import os
 
 import torch
 
@@ -43,12 +44,64 @@ _P, _I, _F, _D = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double
 _lib.register({"ured_adam_clip_step": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _F, _P, _P, _P, _I,
                                        _D, _D, _D, _D, _P, _P, _P]})
 
+_GRAD_VIEWS = os.environ.get("URED_GRAD_VIEWS", "1") == "1"     # A/B knob (tools/gpu_py_ab.sh)
 CHUNK = 8192          # elements per workgroup (never straddles a parameter)
 ALIGN = 16            # each parameter slice starts on a 64-B boundary
 
 
 def _aligned(n):
     return -(-n // ALIGN) * ALIGN
+
+
+def _slot_view(t):
+    """(parameter, its flat-gradient view shaped like t, optimizer) or None."""
+    p = t if t._base is None else t._base
+    slot = getattr(p, "_ured_gslot", None)
+    if not _GRAD_VIEWS or slot is None or p.numel() != t.numel() or not t.is_contiguous():
+        return None
+    opt, o, n = slot
+    if opt.flat_grad is None:
+        return None
+    return p, opt.flat_grad[o:o + n].view(t.shape), opt
+
+
+def grad_slot(t):
+    """Output storage for the gradient of `t` — a parameter, or a same-size view of one (the
+    reshaped conv weights the HIP Functions take) — inside a backward pass: (buffer, accumulate).
+
+    When the parameter lives in a FlatAdam flat buffer and has no gradient yet, the first claim
+    in a backward (one per zero_grad) gets a fresh view of its slice of the flat gradient and
+    accumulate=False: the Function writes the gradient there and returns the view, autograd's
+    AccumulateGrad takes it over as `p.grad` (a fresh, contiguous, layout-matching tensor is
+    stolen, not copied), and gather_grads() finds it in place: no per-step copy into the flat
+    buffer. A second use of the same parameter in the same backward (a layer applied twice, e.g.
+    the cross-attention update of both node sets) gets the same view with accumulate=True: its
+    Function adds its gradient into the view (the kernels' accumulate flag) and returns None for
+    that input, so autograd has no second gradient to add: either p.grad already is the view, or
+    AccumulateGrad has not run yet and will adopt (or copy) the view after this backward's kernels
+    on the same stream. Every other case (no flat layout, gradients kept across backward calls, a
+    double-backward) gets a fresh tensor and accumulate=False: autograd's usual accumulation."""
+    sv = _slot_view(t)
+    if sv is not None and not torch.is_grad_enabled():
+        p, view, opt = sv
+        if p.grad is None and getattr(p, "_ured_gclaim", None) != opt._gen:
+            p._ured_gclaim = opt._gen
+            return view, False
+        if getattr(p, "_ured_gclaim", None) == opt._gen and (p.grad is None or p.grad.data_ptr() == view.data_ptr()):
+            return view, True
+    return torch.empty(t.shape, device=t.device), False
+
+
+def grad_buffer(t):
+    """grad_slot() for callers that cannot accumulate: the flat view on the first claim of a
+    backward, else a fresh tensor (autograd accumulates)."""
+    sv = _slot_view(t)
+    if sv is not None and not torch.is_grad_enabled():
+        p, view, opt = sv
+        if p.grad is None and getattr(p, "_ured_gclaim", None) != opt._gen:
+            p._ured_gclaim = opt._gen
+            return view
+    return torch.empty(t.shape, device=t.device)
 
 
 class FlatAdam(torch.optim.Optimizer):
@@ -61,6 +114,7 @@ class FlatAdam(torch.optim.Optimizer):
         self._lr_t, self._lr_host = None, None
         self._gathered = False
         self._active = None
+        self._gen = 0                   # backward generation (zero_grad count), see grad_buffer()
         self.layout_order = None        # optional: parameter order for the flat layout (see module doc)
 
     # ---- layout -------------------------------------------------------------------------
@@ -81,8 +135,22 @@ class FlatAdam(torch.optim.Optimizer):
         else:
             first = [i for i, p in enumerate(plist) if id(p) in active_ids]
         rest = [i for i in range(len(plist)) if id(plist[i]) not in active_ids]
-        off, total = [0] * len(plist), 0
+        # parameters that declare a chain (`_ured_chain`: a tuple of parameters, e.g. one
+        # attention's in_proj q/k/v weights) are laid out back to back in chain order, from
+        # wherever the first member falls, so that the HIP layers can use them as ONE matrix
+        # (attention_graph/attention_gnn.py; ured_hip.node.fused_rows)
+        seq, placed = [], set()
         for i in first + rest:
+            chain = getattr(plist[i], "_ured_chain", None)
+            members = [rank[id(q)] for q in chain if id(q) in rank] if chain else [i]
+            cls = id(plist[i]) in active_ids
+            for j in members:
+                if j not in placed and (id(plist[j]) in active_ids) == cls:
+                    placed.add(j)
+                    seq.append(j)
+        seq += [i for i in first + rest if i not in placed]
+        off, total = [0] * len(plist), 0
+        for i in seq:
             off[i] = total
             total += _aligned(plist[i].numel())
         self.params_all, self._seg_of, self._off, self._rank = plist, seg_of, off, rank
@@ -96,6 +164,7 @@ class FlatAdam(torch.optim.Optimizer):
             self.flat_param[o:o + n].copy_(p.detach().reshape(-1))
             p.data = self.flat_param[o:o + n].view_as(p)
             self._gviews.append(self.flat_grad[o:o + n].view_as(p))
+            p._ured_gslot = (self, o, n)
         self._nseg = len(self._segments)
         self._coef = torch.ones(self._nseg, device=dev)
         self._lr_t = torch.zeros(1, device=dev)
@@ -198,6 +267,7 @@ class FlatAdam(torch.optim.Optimizer):
     # ---- torch.optim.Optimizer API ------------------------------------------------------
     def zero_grad(self, set_to_none=True):
         self._gathered = False
+        self._gen += 1
         super().zero_grad(set_to_none=set_to_none)
 
     @torch.no_grad()

@@ -186,16 +186,30 @@ def test_node_ffn_and_linear2_match_reference(dev, sets):
     xq = torch.randn(32, C, device=dev, requires_grad=True)
     xk = torch.randn(256, C, device=dev, requires_grad=True)
     Wq, bq = torch.randn(C, C, device=dev, requires_grad=True), torch.randn(C, device=dev, requires_grad=True)
-    Wk, bk = torch.randn(2 * C, C, device=dev, requires_grad=True), torch.randn(2 * C, device=dev, requires_grad=True)
-    q, kv = node.node_linear2(xq, Wq, bq, xk, Wk, bk)
-    gq, gk = torch.randn_like(q), torch.randn_like(kv)
-    (q * gq).sum().backward(retain_graph=True)
-    (kv * gk).sum().backward()
-    ts = [t.detach().double().cpu().requires_grad_(True) for t in (xq, Wq, bq, xk, Wk, bk)]
-    q64 = ts[0] @ ts[1].t() + ts[2]
-    k64 = ts[3] @ ts[4].t() + ts[5]
-    ((q64 * gq.double().cpu()).sum() + (k64 * gk.double().cpu()).sum()).backward()
-    _close(q, q64)
-    _close(kv, k64)
-    for a, b in zip((xq, Wq, bq, xk, Wk, bk), ts):
-        _close(a.grad, b.grad, 2e-5)
+    # k and v weights / biases: adjacent slices of one buffer (the FlatAdam layout, read as one
+    # matrix) or separate tensors (concatenated inside the Function)
+    for adjacent in (True, False):
+        if adjacent:
+            wbuf, bbuf = torch.randn(2 * C * C, device=dev), torch.randn(2 * C, device=dev)
+            Wk1, Wk2 = (wbuf[i * C * C:(i + 1) * C * C].view(C, C).detach().requires_grad_(True) for i in (0, 1))
+            bk1, bk2 = (bbuf[i * C:(i + 1) * C].detach().requires_grad_(True) for i in (0, 1))
+            assert node.fused_rows([Wk1, Wk2]) is not None
+        else:
+            Wk1, Wk2 = (torch.randn(C, C, device=dev, requires_grad=True) for _ in (0, 1))
+            bk1, bk2 = (torch.randn(C, device=dev, requires_grad=True) for _ in (0, 1))
+            assert node.fused_rows([Wk1, Wk2]) is None
+        for t in (xq, xk, Wq, bq):
+            t.grad = None
+        q, kv = node.node_proj((xq, xk), [(Wq,), (Wk1, Wk2)], [(bq,), (bk1, bk2)])
+        gq, gk = torch.randn_like(q), torch.randn_like(kv)
+        (q * gq).sum().backward(retain_graph=True)
+        (kv * gk).sum().backward()
+        leaves = (xq, Wq, bq, xk, Wk1, Wk2, bk1, bk2)
+        ts = [t.detach().double().cpu().requires_grad_(True) for t in leaves]
+        q64 = ts[0] @ ts[1].t() + ts[2]
+        k64 = ts[3] @ torch.cat([ts[4], ts[5]]).t() + torch.cat([ts[6], ts[7]])
+        ((q64 * gq.double().cpu()).sum() + (k64 * gk.double().cpu()).sum()).backward()
+        _close(q, q64)
+        _close(kv, k64)
+        for a, b in zip(leaves, ts):
+            _close(a.grad, b.grad, 2e-5)

@@ -22,8 +22,9 @@ import attention_graph.attention_gnn as agn  # noqa: E402
 if "seq" in sys.argv:
     orig = node.launch
     node.launch = lambda *ds: [orig(d) for d in ds]
-if "nolin2" in sys.argv:
-    agn.node_linear2 = lambda x1, W1, b1, x2, W2, b2: (node.node_linear(x1, W1, b1), node.node_linear(x2, W2, b2))
+if "noproj" in sys.argv:    # each projection group as its own launch
+    agn.node_proj = lambda xs, ws, bs: tuple(node.node_proj((x,), [w], [b]) for x, w, b in zip(xs, ws, bs)) \
+        if len(xs) > 1 else node.node_proj(xs, ws, bs)
 if "noffn" in sys.argv:
     agn.ResidualAttentionMessagePropagation._node_ffn_ok = lambda self: False
 if "nopd" in sys.argv:
