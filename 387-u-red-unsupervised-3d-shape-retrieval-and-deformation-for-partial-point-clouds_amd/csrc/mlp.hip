@@ -211,6 +211,15 @@ template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; }
 #ifndef URED_BNBWD_YALL
 #define URED_BNBWD_YALL 1
 #endif
+// gemm2 BN-backward epilogue: the previous layer's output tile Yp reaches LDS by DMA during the
+// last K-step (rows 0-63 into the free stage buffer, rows 64-127 into the consumed one once every
+// wave has read its fragments), so its HBM latency hides under that step's MFMAs. Measured
+// neutral on the config-2 step (dgrad 3.63 vs 3.56 ms/step, 62.0 vs 62.1 it/s, same-box A/B,
+// tools/gpu_lib_ab.sh): the co-resident block already covers the epilogue's latency. Off; kept
+// for experiments (it lowers the kernel's VGPR count 193 -> 175).
+#ifndef URED_YP_LDS
+#define URED_YP_LDS 0
+#endif
 
 // ---- shared epilogue ---------------------------------------------------------
 // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
@@ -287,9 +296,10 @@ struct InTile {
     }
 };
 
-template <int EPI, bool BUFST = false, class Pre = NoPre>
+template <int EPI, bool BUFST = false, bool YL = false, class Pre = NoPre>
 __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2], int m0, int n0,
-                                         float* red_f, int* red_i, Pre pre = Pre()) {
+                                         float* red_f, int* red_i, Pre pre = Pre(),
+                                         const float* yl0 = nullptr, const float* yl1 = nullptr) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
     // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
     const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
@@ -487,7 +497,9 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         // the fragment registers are dead, so the whole tile fits without raising the kernel's
         // VGPR peak, and the epilogue then waits for one HBM round trip instead of two (gfx9
         // vmcnt is in order: the second half's loads otherwise queue behind the first half's stores)
-        f16v yh[URED_BNBWD_YALL ? 2 : 1][2];
+        // YL: the tile's Yp rows are in LDS (yl0: rows 0-63, yl1: rows 64-127; 128 floats per row)
+        constexpr bool YG = !YL;               // Yp read from global into registers
+        f16v yh[(URED_BNBWD_YALL || !YG) ? 2 : 1][2];
         InTile<BUFST> Yr(d.Yp, d.ldy, d.M, d.N);
         auto load_y = [&](int j) {
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
@@ -496,7 +508,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
 #pragma unroll
                 for (int r = 0; r < 16; ++r) yh[URED_BNBWD_YALL ? j : 0][i][r] = Yr.get(row_of(i, r), col);
         };
-        if (!URED_BNBWD_YALL) load_y(0);
+        if (YG && !URED_BNBWD_YALL) load_y(0);
         // max-pool backward: the pooled gradient lands on the winning row of each (group, column)
         const bool pool_blk = d.pool_idx && (d.pool_group_rows % BM == 0);
         const int pg = pool_blk ? m0 / d.pool_group_rows : 0;
@@ -511,7 +523,21 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             pidx_[j] = -1; pgr_[j] = 0.f;
             if (pool_blk && cv) { pidx_[j] = d.pool_idx[(size_t)pg * d.N + col]; pgr_[j] = d.pool_grad[(size_t)pg * d.N + col]; }
         }
-        if (URED_BNBWD_YALL) { load_y(0); load_y(1); }   // behind the (L2-resident) per-column parameters
+        if (YG && URED_BNBWD_YALL) { load_y(0); load_y(1); }   // behind the (L2-resident) per-column parameters
+        if constexpr (YL) {
+            // this wave's Yp DMA (and the parameters) landed, then every wave's
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_barrier();
+            const float* yb = wm ? yl1 : yl0;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        yh[j][i][r] = yb[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * BN + wn * 64 + j * 32 +
+                                         (lane & 31)];
+        }
         pre();
         OutTile<BUFST> Gw(d.C, d.ldc, d.M, d.N);
         // per-element global reads (a residual gradient, or pooled gradients of groups that do
@@ -521,7 +547,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         const float ylo = d.bwd_res == URED_ACT_RES ? 0.f : -__builtin_inff();
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            if (!URED_BNBWD_YALL && j == 1) load_y(1);
+            if (YG && !URED_BNBWD_YALL && j == 1) load_y(1);
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
             const bool cv = col < d.N;
             const float sc = sc_[j], sh = sh_[j], mu = mu_[j], is = is_[j];
@@ -541,7 +567,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                         const bool ok = cv && row < d.M;
                         const float a = acc[i][j][r];
                         const float dh = (row == pidx) ? a + pgr : a;
-                        const float y = yh[URED_BNBWD_YALL ? j : 0][i][r];
+                        const float y = yh[(URED_BNBWD_YALL || YL) ? j : 0][i][r];
                         const float xh = (fmaxf(y, ylo) - mu) * is;
                         const float g = (__builtin_fmaf(y, sck, shk) > 0.f) ? dh : 0.f;
                         Gw.put(ok, row, col, g);
@@ -563,7 +589,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                         if (d.pool_idx[ge] == row) dh += d.pool_grad[ge];
                     }
                     if (d.gadd && ok) dh += d.gadd[(size_t)row * d.ldg + col];
-                    const float y = yh[URED_BNBWD_YALL ? j : 0][i][r];
+                    const float y = yh[(URED_BNBWD_YALL || YL) ? j : 0][i][r];
                     float g, xh;
                     if (d.bwd_res == URED_ACT_RES) {
                         g = dh;
@@ -884,6 +910,26 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     setup(m0, n0);
     if (has_k) issue(0, kbeg, m0, n0);
 
+    // BN-backward epilogue input Yp by LDS-DMA (URED_YP_LDS): tile row 64hh + 2(8w + q) + (lane>>5),
+    // columns 4(lane&31) .. +3, into stage buffer st at byte (8w + q) KB + 16 lane (row-major,
+    // 128 floats per row). Rows past M read as zeros (descriptor bound); never stored.
+    constexpr bool YPL = URED_YP_LDS && EPI == URED_EPI_BNBWD && !GEMM_PERSIST;
+    i32x4 yrs = {0, 0, 0, 0};
+    unsigned yvo = 0;
+    const unsigned smem_b = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem);
+    if constexpr (YPL) {
+        yrs = make_rsrc(d.Yp, ((long long)(d.M - 1) * d.ldy + d.N) * 4);
+        yvo = (unsigned)(((long long)(m0 + h) * d.ldy + n0 + 4 * li) * 4);
+    }
+    auto yp_dma = [&](int hh, int st) {
+        const unsigned ld8 = (unsigned)d.ldy * 8u;            // two rows per DMA instruction
+        const unsigned b = yvo + (unsigned)(hh * 64 + w * 16) * (unsigned)d.ldy * 4u;
+        const unsigned l = __builtin_amdgcn_readfirstlane(smem_b + (unsigned)st * (2u * TILE * 4u) + (unsigned)w * 8192u);
+        dma4(yrs, b, b + ld8, b + 2u * ld8, b + 3u * ld8, l);
+        dma4(yrs, b + 4u * ld8, b + 5u * ld8, b + 6u * ld8, b + 7u * ld8, l + 4096u);
+    };
+
     while (true) {
         f16v acc[2][2];
 #pragma unroll
@@ -1021,6 +1067,11 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                 acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][j], acc[1][1], 0, 0, 0);
                 if (URED_DMA_SPREAD && next && j == 1) issue_a(stage ^ 1, k0 + BK);
                 if (URED_DMA_SPREAD && next && j == 5) issue_b(stage ^ 1, k0 + BK);
+                if (YPL && !next && j == 1) yp_dma(0, stage ^ 1);
+                if (YPL && !next && j == 8) {     // every wave has its fragments: `stage` is free
+                    lds_barrier();
+                    yp_dma(1, stage);
+                }
             }
             stage ^= 1;
         }
@@ -1036,7 +1087,9 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                 if (has_k) issue(stage, kbeg, nm0, nn0);
             }
         };
-        epilogue<EPI, true>(d, acc, m0, n0, red_f, red_i, pre);
+        if (YPL && !has_k) { yp_dma(0, stage); yp_dma(1, stage ^ 1); }
+        epilogue<EPI, true, YPL>(d, acc, m0, n0, red_f, red_i, pre, smem + stage * 2 * TILE,
+                                 smem + (stage ^ 1) * 2 * TILE);
         if (!GEMM_PERSIST || nv >= ntiles) break;
         v = nv; m0 = nm0; n0 = nn0;
         after_epi = true;

@@ -633,6 +633,39 @@ __global__ __launch_bounds__(DCD_THREADS) void dcd_kernel(const float* __restric
     }
 }
 
+// ---- get_part regrouping backward (ured_part_rows_bwd) ---------------------------------------
+// Row-wise gather: each block covers rows_per_block output rows (C/V vector lanes per row), reads
+// the sorted-row gradient and the part-sum gradient of the row's sorted position once each (V
+// floats per lane) and writes the sum. HBM-bound: 2 reads + 1 write of R x C floats.
+template <int V>
+__global__ __launch_bounds__(256) void part_rows_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ dsum,
+                                                            const long long* __restrict__ inv,
+                                                            const int* __restrict__ gid, int N, int C, long long rows,
+                                                            int rows_per_block, float* __restrict__ out) {
+    const int per_row = C / V;
+    const int lr = threadIdx.x / (per_row < 256 ? per_row : 256);
+    if (lr >= rows_per_block) return;
+    const long long r = (long long)blockIdx.x * rows_per_block + lr;
+    if (r >= rows) return;
+    const long long b = r / N;
+    const long long s = b * N + inv[r];
+    const long long g = gid[s];
+    for (int c = threadIdx.x - lr * (per_row < 256 ? per_row : 256); c < per_row; c += 256) {
+        if constexpr (V == 4) {
+            float4 v = ds ? reinterpret_cast<const float4*>(ds + s * C)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (dsum) {
+                const float4 u = reinterpret_cast<const float4*>(dsum + g * C)[c];
+                v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+            }
+            reinterpret_cast<float4*>(out + r * C)[c] = v;
+        } else {
+            float v = ds ? ds[s * C + c] : 0.f;
+            if (dsum) v += dsum[g * C + c];
+            out[r * C + c] = v;
+        }
+    }
+}
+
 // ---- per-part axis-aligned boxes (compute_aabbox, dataset/dataset_utils.py:77-85) ---------
 // One workgroup per segment of the label-sorted points: min / max of each coordinate (exact,
 // order-independent), then (center, half extent) = ((lo+hi)/2, (hi-lo)/2). Empty segments
@@ -862,6 +895,27 @@ int ured_seg_aabb(const float* x, const int* off, int G, float* out, void* strea
     URED_REQUIRE(G <= (1 << 30), "ured_seg_aabb: too many segments");
     hipLaunchKernelGGL(seg_aabb_kernel, dim3(G), dim3(256), 0, (hipStream_t)stream, x, off, out);
     return ured::launch_status("ured_seg_aabb");
+}
+
+int ured_part_rows_bwd(const float* d_sorted, const float* d_sums, const long long* inv, const int* gid, int B, int N,
+                       int C, float* out, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(B >= 0 && N >= 0 && C >= 0, "ured_part_rows_bwd: negative size");
+    if (B == 0 || N == 0 || C == 0) return 0;
+    URED_REQUIRE(inv && gid && out, "ured_part_rows_bwd: null pointer");
+    URED_REQUIRE((long long)B * N * C < (1LL << 40), "ured_part_rows_bwd: too large");
+    const bool vec = C % 4 == 0 && (((uintptr_t)out | (uintptr_t)d_sorted | (uintptr_t)d_sums) & 15) == 0;
+    const long long rows = (long long)B * N;
+    const int per_row = vec ? C / 4 : C;
+    const int rows_per_block = per_row >= 256 ? 1 : 256 / per_row;
+    const unsigned grid = (unsigned)((rows + rows_per_block - 1) / rows_per_block);
+    if (vec)
+        hipLaunchKernelGGL(part_rows_bwd_kernel<4>, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_sorted, d_sums, inv,
+                           gid, N, C, rows, rows_per_block, out);
+    else
+        hipLaunchKernelGGL(part_rows_bwd_kernel<1>, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_sorted, d_sums, inv,
+                           gid, N, C, rows, rows_per_block, out);
+    return ured::launch_status("ured_part_rows_bwd");
 }
 
 int ured_dcd(const float* dist1, const int* idx1, const float* dist2, const int* idx2, int b, int n1, int n2,

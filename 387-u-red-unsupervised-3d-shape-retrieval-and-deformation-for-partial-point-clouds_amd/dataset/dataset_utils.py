@@ -40,11 +40,20 @@ def get_shape(A, param, src_default_param=None, weight=1.0, param_init=None, con
     return torch.bmm(A, p).reshape(bs, num_part, -1, 3)
 
 
+_MIRROR = {}
+
+
 def get_symmetric(pc):
-    """x -> -x reflection (dataset_utils.py:1194-1196). Built without a host-made constant
-    tensor (an H2D copy is not allowed inside HIP-graph capture); negation is exact, so the
-    values equal the reference's multiply by [-1, 1, 1]."""
-    return torch.cat((-pc[..., :1], pc[..., 1:]), dim=-1)
+    """x -> -x reflection (dataset_utils.py:1194-1196): the reference's multiply by [-1, 1, 1]
+    (one kernel each way). The constant is made on the device by fills on first use (an H2D copy
+    is not allowed inside HIP-graph capture) and cached per device and dtype."""
+    key = (pc.device, pc.dtype)
+    s = _MIRROR.get(key)
+    if s is None:
+        s = torch.ones(3, device=pc.device, dtype=pc.dtype)
+        s[0] = -1.0
+        _MIRROR[key] = s
+    return pc * s
 
 
 def _index(source_labels, db):

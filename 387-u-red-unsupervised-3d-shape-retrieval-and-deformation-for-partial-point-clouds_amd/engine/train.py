@@ -49,7 +49,7 @@ from network.simple_encoder import TargetEncoder as simple_encoder  # noqa: E402
 from train_utils.load_sources import load_sources  # noqa: E402
 from train_utils.optimizer_dm import define_optimizer_dm_re_recon  # noqa: E402
 from ured_hip.kernels import RowWeights  # noqa: E402
-from ured_hip.ops import UniqueRows, build_parts, part_aabb, permute_rows, segment_sum  # noqa: E402
+from ured_hip.ops import UniqueRows, build_parts, part_aabb, part_rows  # noqa: E402
 
 MODULE_NAMES = ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "re_residual_net_full",
                 "src_encoder_all", "recon_decoder_src", "embedding_layer")
@@ -103,8 +103,7 @@ def get_part(cfg, per_point_full, target_labels, x):
     B, N, C = per_point_full.shape
     P = cfg["MAX_NUM_PARTS"]
     parts = build_parts(target_labels, x, P)
-    pp_sorted = permute_rows(per_point_full, parts.perm, parts.inv_perm).reshape(B * N, C)
-    sums = segment_sum(pp_sorted, parts.off, parts.gid)
+    pp_sorted, sums = part_rows(per_point_full, parts)
     part_mean = sums / parts.counts.reshape(-1, 1).clamp(min=1).float()
     aabb = part_aabb(parts)                                            # by part slot (rank)
     param_def = torch.gather(aabb, 1, parts.rank_of_label.clamp(min=0).unsqueeze(-1).expand(-1, -1, 6))

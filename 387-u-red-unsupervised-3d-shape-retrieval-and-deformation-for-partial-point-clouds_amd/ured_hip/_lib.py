@@ -28,6 +28,7 @@ _SIGNATURES = {
     "ured_nn_seg_fwd": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_nn_fwd_workspace": [_I, _I, _I, _I, _I, _I],
     "ured_seg_aabb": [_P, _P, _I, _P, _P],
+    "ured_part_rows_bwd": [_P, _P, _P, _P, _I, _I, _I, _P, _P],
     "ured_get_shape_fwd": [_P, _P, _I, _I, _P, _P],
     "ured_get_shape_bwd": [_P, _P, _I, _I, _P, _P],
     "ured_emd_workspace": [_I, _I],

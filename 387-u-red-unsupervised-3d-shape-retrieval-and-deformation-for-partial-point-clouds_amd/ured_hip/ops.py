@@ -75,6 +75,41 @@ def permute_rows(x, perm, inv):
     return PermuteRowsFn.apply(x, perm, inv)
 
 
+class PartRowsFn(Function):
+    """get_part's regrouping of per-point features (engine/train.py:103-136): x [B, N, C] ->
+    (rows sorted by part label [B*N, C], per-part-slot sums [G, C]). Forward: one gather and one
+    HIP segment sum; backward: ONE HIP pass (ured_part_rows_bwd) where the separate ops would
+    take an index_select of the part gradients, an add and the inverse-permutation gather."""
+
+    @staticmethod
+    def forward(ctx, x, perm, inv, off, gid):
+        B, N, C = x.shape
+        xs = torch.gather(x, 1, perm.unsqueeze(-1).expand(-1, -1, C)).reshape(B * N, C)
+        sums = K.group_colsum(xs, C, off.shape[0] - 1, off=off)
+        ctx.save_for_backward(inv, gid)
+        ctx.shape = (B, N, C)
+        return xs, sums
+
+    @staticmethod
+    def backward(ctx, d_sorted, d_sums):
+        inv, gid = ctx.saved_tensors
+        B, N, C = ctx.shape
+        ds = None if d_sorted is None else d_sorted.contiguous()
+        dg = None if d_sums is None else d_sums.contiguous()
+        if inv.dtype != torch.int64 or gid.dtype != torch.int32:
+            raise TypeError("part_rows: inv must be int64 and gid int32")
+        out = torch.empty(B, N, C, device=inv.device)
+        _lib.call("ured_part_rows_bwd", _lib.ptr(ds), _lib.ptr(dg), _lib.ptr(inv.contiguous()), _lib.ptr(gid.contiguous()),
+                  B, N, C, _lib.ptr(out), _lib.stream_of(out))
+        return out, None, None, None, None
+
+
+def part_rows(x, parts):
+    """(x regrouped by part [B*N, C], per-part-slot sums [B*P, C]) for a PartBatch."""
+    _lib.require_device(x)
+    return PartRowsFn.apply(x, parts.perm, parts.inv_perm, parts.off, parts.gid)
+
+
 def segment_sum(x, off, gid):
     """x [R, C], off int32 [G+1] (row ranges), gid int32 [R] (segment of each row) -> [G, C]."""
     return SegmentSumFn.apply(x, off, gid)

@@ -103,6 +103,14 @@ int ured_get_shape_bwd(const float* A, const float* grad_out, int nparts, int ro
  * offsets -> out [G,6] = (center, half extent) of each segment; empty segments give zeros. */
 int ured_seg_aabb(const float* x, const int* off, int G, float* out, void* stream);
 
+/* Backward of get_part's per-point regrouping (engine/train.py:103-136: the points of every
+ * sample sorted by part label, and the per-part sums of their features): for R = B*N rows of C
+ * floats, out[b*N + i] = d_sorted[s] + d_sums[gid[s]] with s = b*N + inv[b, i] (the row's
+ * position after the sort, inv int64 [B, N]; gid int32 [R] the part slot of each sorted row).
+ * Either gradient may be NULL (zero). One pass: replaces an index_select, a gather and an add. */
+int ured_part_rows_bwd(const float* d_sorted, const float* d_sums, const long long* inv, const int* gid, int B, int N,
+                       int C, float* out, void* stream);
+
 /* ---------------- EMD (auction algorithm) ---------------- */
 /* Approximate EMD matching of xyz1 [b,n,3] to xyz2 [b,n,3] (reference emd.forward,
  * utils_v2/metrics/EMD/emd.cpp:14-19 -> emd_cuda.cu:183-256): `iters` auction rounds with

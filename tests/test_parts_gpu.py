@@ -59,3 +59,32 @@ def test_get_shape_hip_matches_bmm(dev):
     prm.grad = None
     get_shape(A, prm, dflt, 0.1).backward(go)
     assert torch.equal(prm.grad, g1)
+
+
+@pytest.mark.parametrize("B,N,P,C,kmax", [(16, 2048, 16, 512, 4), (3, 700, 16, 6, 16), (2, 5, 8, 3, 8)])
+def test_part_rows_matches_separate_ops(dev, B, N, P, C, kmax):
+    """PartRowsFn (gather by part label + per-part sums, one-pass HIP backward) vs the separate
+    ops it replaces (permute_rows + segment_sum, autograd's index_select / add / gather):
+    forward and backward bit-identical (the backward's one add is commutative)."""
+    from ured_hip.ops import build_parts, part_rows, permute_rows, segment_sum
+    g = torch.Generator().manual_seed(B * N + C)
+    x = torch.randn(B, N, C, generator=g).to(dev)
+    labels = torch.randint(0, kmax, (B, N), generator=g).to(dev)
+    parts = build_parts(labels, torch.randn(B, N, 3, generator=g).to(dev), P)
+    gs = torch.randn(B * N, C, generator=g).to(dev)
+    gp = torch.randn(B * P, C, generator=g).to(dev)
+    for use in ((True, True), (True, False), (False, True)):
+        a = x.clone().requires_grad_(True)
+        xs, sums = part_rows(a, parts)
+        b = x.clone().requires_grad_(True)
+        xs2 = permute_rows(b, parts.perm, parts.inv_perm).reshape(B * N, C)
+        sums2 = segment_sum(xs2, parts.off, parts.gid)
+        assert torch.equal(xs, xs2) and torch.equal(sums, sums2)
+        xs_g = xs if use[0] else xs.detach()
+        sums_g = sums if use[1] else sums.detach()
+        outs = [t for t, u in ((xs_g, use[0]), (sums_g, use[1])) if u]
+        grads = [t for t, u in ((gs, use[0]), (gp, use[1])) if u]
+        torch.autograd.backward(outs, grads)
+        outs2 = [t for t, u in ((xs2, use[0]), (sums2, use[1])) if u]
+        torch.autograd.backward(outs2, grads)
+        assert torch.equal(a.grad, b.grad), (a.grad - b.grad).abs().max().item()

@@ -37,6 +37,8 @@ class Census(TorchDispatchMode):
         if name not in SKIP:
             where = "backward/autograd"
             for fr in reversed(traceback.extract_stack()[:-1]):
+                if "op_census" in fr.filename:
+                    continue
                 if PKG in fr.filename or "/tools/" in fr.filename or "/engine/" in fr.filename:
                     where = f"{os.path.relpath(fr.filename, ROOT)}:{fr.lineno} {fr.name}"
                     break
