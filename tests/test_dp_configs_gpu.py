@@ -62,12 +62,19 @@ def _worker(rank, world, port, bs, npts, q):
         ok_avg, losses, worst = True, [], 0.0
         for it in range(2):
             batch = batch_to_device(synthetic.make_batch(bs, npts, 512, parts=4, seed=100 * it + rank), dev)
+            # the rank's local gradient first (hooks not armed: nothing is reduced), then the same
+            # step again with the reduction (gradients land in the flat buffer that the hooks
+            # all-reduce in place during backward, as DDP does; training-mode BN makes the second
+            # forward's values identical)
+            step.optimizer.zero_grad(set_to_none=True)
+            loss, _ = step.forward(batch, 1)
+            loss.backward()
+            local = {id(p): p.grad.detach().clone() for p in step.params if p.grad is not None}
             step.optimizer.zero_grad(set_to_none=True)
             loss, _ = step.forward(batch, 1)
             if step.reducer is not None:
                 step.reducer.begin()               # step 2: buckets all-reduced from backward's hooks
             loss.backward()
-            local = {id(p): p.grad.detach().clone() for p in step.params if p.grad is not None}
             step.reduce_gradients()
             for p in step.params:
                 if id(p) not in local:
