@@ -116,7 +116,13 @@ __device__ __forceinline__ void load_chunk(const LaneSrc& sa, const LaneSrc& sb,
     ld16(sb, bkc, kb, K, false, b);
 }
 
-__global__ __launch_bounds__(NG_NT) void node_gemm_kernel(const NodeJobs jobs) {
+#ifndef URED_NODE_WG_PER_CU
+#define URED_NODE_WG_PER_CU 2
+#endif
+// two workgroups per CU (the second launch-bounds argument is waves per SIMD: 4 -> <= 128 VGPRs;
+// one accumulator chain per wave, the four waves of a SIMD interleave their MFMAs), so a launch
+// of a few hundred tiles runs in one round
+__global__ __launch_bounds__(NG_NT, URED_NODE_WG_PER_CU * NG_WAVES / 4) void node_gemm_kernel(const NodeJobs jobs) {
     __shared__ float red[NG_WAVES * NG_BM * NG_BN];      // 32 KB: the 8 waves' partial tiles
     int ji = 0;
 #pragma unroll
@@ -148,7 +154,9 @@ __global__ __launch_bounds__(NG_NT) void node_gemm_kernel(const NodeJobs jobs) {
     const int m0 = (tile / J.ntn) * NG_BM, n0 = (tile % J.ntn) * NG_BN;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63, h = lane >> 5, li = lane & 31;
     const bool akc = J.akc, bkc = J.bkc;
-    // two accumulators (even / odd k-steps): independent MFMA chains, summed at the end
+    // URED_NODE_WG_PER_CU 1: two accumulators (even / odd k-steps), independent MFMA chains
+    // summed at the end; 2: one chain (registers for the second resident workgroup)
+    constexpr bool TWO_ACC = URED_NODE_WG_PER_CU == 1;
     f16v acc0, acc1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
@@ -161,22 +169,31 @@ __global__ __launch_bounds__(NG_NT) void node_gemm_kernel(const NodeJobs jobs) {
     if (c < nch) load_chunk(sa, sb, akc, bkc, c * NG_BK, h, d.K, a, b);
     while (c < nch) {
         const int cn = c + NG_WAVES;
-        if (cn < nch) load_chunk(sa, sb, akc, bkc, cn * NG_BK, h, d.K, an, bn);
+        // one chunk of prefetch with one resident workgroup; with two, the other waves of the
+        // SIMD cover the load latency and the registers go to occupancy
+        if (TWO_ACC && cn < nch) load_chunk(sa, sb, akc, bkc, cn * NG_BK, h, d.K, an, bn);
+        if constexpr (TWO_ACC) {
 #pragma unroll
-        for (int j = 0; j < 16; j += 2) {
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j + 1], b[j + 1], acc1, 0, 0, 0);
+            for (int j = 0; j < 16; j += 2) {
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j + 1], b[j + 1], acc1, 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc0, 0, 0, 0);
         }
-        if (cn < nch) {
+        if (TWO_ACC && cn < nch) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) { a[j] = an[j]; b[j] = bn[j]; }
+        } else if (!TWO_ACC && cn < nch) {
+            load_chunk(sa, sb, akc, bkc, cn * NG_BK, h, d.K, a, b);
         }
         c = cn;
     }
     // partial tile -> LDS [wave][row][col]; element r: row (r&3) + 8(r>>2) + 4h, col li
     float* mine = red + w * NG_BM * NG_BN;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) mine[((r & 3) + 8 * (r >> 2) + 4 * h) * NG_BN + li] = acc0[r] + acc1[r];
+    for (int r = 0; r < 16; ++r) mine[((r & 3) + 8 * (r >> 2) + 4 * h) * NG_BN + li] = TWO_ACC ? acc0[r] + acc1[r] : acc0[r];
     __syncthreads();
     // 512 threads x 2 outputs: row t/16, columns 2(t%16), +1; waves summed in fixed order
     const int row = t >> 4, cq = (t & 15) * 2;
