@@ -15,8 +15,11 @@ batch encodes every slot), the residual-loss gate `epoch > init_p_m_loss`): one 
 graph per key, captured the first time the key
 is seen, right after that batch's step runs eagerly (so no extra optimizer step is taken and
 the capture finds libraries and workspaces initialised). At most `max_graphs` are kept (LRU).
-Gradients live in persistent tensors that every graph zeroes and accumulates into, so the one
-update graph serves all of them. When the gate flips, the set of parameters with a gradient
+Gradients live in persistent memory, so the one update graph serves all of them: with FlatAdam
+(the GPU default) the HIP layers write every gradient straight into its slice of the flat
+gradient (ured_hip.optim.grad_slot), so each step starts from `p.grad = None` (no kernel) and
+nothing is zeroed or added; with torch's optimizers the persistent gradient tensors are zeroed
+and autograd accumulates into them. When the gate flips, the set of parameters with a gradient
 changes (re_residual_net_full joins): every graph, the update graph and the persistent
 gradients are dropped and the next step runs eagerly again.
 
@@ -72,13 +75,23 @@ class GraphedStep:
         uq = batch.get("src_unique")
         return (None if uq is None else uq.U, self.gate(epoch))
 
+    def _flat(self):
+        """FlatAdam: the HIP layers write the gradients into its persistent flat buffer."""
+        return hasattr(self.inner.optimizer, "flat_grad")
+
+    def _fresh_grads(self):
+        if self._flat():
+            self.inner.optimizer.zero_grad(set_to_none=True)   # the layers overwrite the flat views
+        else:
+            torch._foreach_zero_(self.grads)                    # keep the persistent grad tensors
+
     def _eager(self, batch, epoch):
         if self.grads is None:                       # first step: torch allocates the grads
             T = self.inner.step(batch, epoch)
             params = [p for m in self.inner.models.values() for p in m.parameters() if p.grad is not None]
             self.grads = [p.grad for p in params]
             return _detached(T)
-        torch._foreach_zero_(self.grads)             # keep the persistent grad tensors
+        self._fresh_grads()
         loss, T = self.inner.forward(batch, epoch)
         loss.backward()
         del loss
@@ -90,8 +103,12 @@ class GraphedStep:
         static = _clone_batch(batch)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        flat = self._flat()
+        if flat:
+            self.inner.optimizer.zero_grad(set_to_none=True)
         with torch.cuda.graph(g):
-            torch._foreach_zero_(self.grads)
+            if not flat:
+                torch._foreach_zero_(self.grads)
             loss, T = self.inner.forward(static, epoch)
             loss.backward()
         T = _detached(T)
