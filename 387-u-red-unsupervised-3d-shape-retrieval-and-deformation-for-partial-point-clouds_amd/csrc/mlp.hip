@@ -221,6 +221,14 @@ template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; }
 #define URED_YP_LDS 0
 #endif
 
+// BN partials (EPI_FWD stat_ws {mean, M2}, EPI_BNBWD bwd_ws {sum g, sum g*xhat}): layout
+// [2][N][nblk], nblk = ceil(M/128) — one column's block partials are contiguous, so the
+// finalizes read them coalesced (the epilogues' few scattered 4-B writes per block are cheap)
+__host__ __device__ __forceinline__ size_t part_idx(int q, int col, int blk, int N, int M) {
+    const int nblk = (M + 127) / 128;
+    return ((size_t)q * N + col) * nblk + blk;
+}
+
 // ---- shared epilogue ---------------------------------------------------------
 // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
 #define RED(a, q, c) red_f[((a) * 2 + (q)) * BN + (c)]
@@ -432,8 +440,8 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                 const int c = wn * 64 + j * 32 + lane;
                 const int col = n0 + c;
                 if (col < d.N) {
-                    d.stat_ws[(size_t)blk * 2 * d.N + col] = cmean[j];
-                    d.stat_ws[(size_t)blk * 2 * d.N + d.N + col] = RED(0, 1, c) + RED(1, 1, c);
+                    d.stat_ws[part_idx(0, col, blk, d.N, d.M)] = cmean[j];
+                    d.stat_ws[part_idx(1, col, blk, d.N, d.M)] = RED(0, 1, c) + RED(1, 1, c);
                 }
             }
         }
@@ -624,8 +632,8 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                 const int c = wn * 64 + j * 32 + lane;
                 const int col = n0 + c;
                 if (col < d.N) {
-                    d.bwd_ws[(size_t)blk * 2 * d.N + col] = RED(0, 0, c) + RED(1, 0, c);
-                    d.bwd_ws[(size_t)blk * 2 * d.N + d.N + col] = RED(0, 1, c) + RED(1, 1, c);
+                    d.bwd_ws[part_idx(0, col, blk, d.N, d.M)] = RED(0, 0, c) + RED(1, 0, c);
+                    d.bwd_ws[part_idx(1, col, blk, d.N, d.M)] = RED(0, 1, c) + RED(1, 1, c);
                 }
             }
         }
@@ -1263,7 +1271,7 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
     double s = 0.0, c = 0.0;
     for (int b = t; b < nblk; b += 256) {
         const double cnt = (double)min(BM, M - b * BM) * blk_weight(gw, grows, b);
-        s += cnt * (double)ws[(size_t)b * 2 * N + n];
+        s += cnt * (double)ws[part_idx(0, n, b, N, M)];
         c += cnt;
     }
     sh[t] = s;
@@ -1277,8 +1285,8 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
     for (int b = t; b < nblk; b += 256) {
         const double w = blk_weight(gw, grows, b);
         const double cnt = (double)min(BM, M - b * BM) * w;
-        const double dm = (double)ws[(size_t)b * 2 * N + n] - mean;
-        q += w * (double)ws[(size_t)b * 2 * N + N + n] + cnt * dm * dm;
+        const double dm = (double)ws[part_idx(0, n, b, N, M)] - mean;
+        q += w * (double)ws[part_idx(1, n, b, N, M)] + cnt * dm * dm;
     }
     sh[t] = q;
     __syncthreads();
@@ -1311,8 +1319,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     const int nblk = (M + BM - 1) / BM;
     double a = 0.0, b = 0.0, c = 0.0;
     for (int k = t; k < nblk; k += 256) {
-        a += (double)ws[(size_t)k * 2 * N + n];
-        b += (double)ws[(size_t)k * 2 * N + N + n];
+        a += (double)ws[part_idx(0, n, k, N, M)];
+        b += (double)ws[part_idx(1, n, k, N, M)];
         c += (double)min(BM, M - k * BM) * blk_weight(gw, grows, k);
     }
     s1[t] = a; s2[t] = b; s3[t] = c;
@@ -1629,8 +1637,8 @@ __global__ __launch_bounds__(SMALL_NT) void dgrad_small_bnbwd_kernel(const UredG
     if (t < N) {
         float s1 = 0.f, s2 = 0.f;
         for (int q = 0; q < rg; ++q) { s1 += red[0][q * N + t]; s2 += red[1][q * N + t]; }
-        d.bwd_ws[(size_t)blockIdx.x * 2 * N + t] = s1;
-        d.bwd_ws[(size_t)blockIdx.x * 2 * N + N + t] = s2;
+        d.bwd_ws[part_idx(0, t, blockIdx.x, N, d.M)] = s1;
+        d.bwd_ws[part_idx(1, t, blockIdx.x, N, d.M)] = s2;
     }
 }
 
@@ -1694,8 +1702,8 @@ __global__ __launch_bounds__(SMALL_NT) void fwd_small_stats_kernel(const UredGem
     if (t < N) {
         float sum = 0.f;
         for (int q = 0; q < rg; ++q) sum += red[q * N + t];
-        d.stat_ws[(size_t)blockIdx.x * 2 * N + t] = cmean[t];
-        d.stat_ws[(size_t)blockIdx.x * 2 * N + N + t] = sum;
+        d.stat_ws[part_idx(0, t, blockIdx.x, N, d.M)] = cmean[t];
+        d.stat_ws[part_idx(1, t, blockIdx.x, N, d.M)] = sum;
     }
 }
 

@@ -162,7 +162,7 @@ int ured_dcd(const float* dist1, const int* idx1, const float* dist2, const int*
  *   EPI_STORE : C = acc (+bias[n])
  *   EPI_FWD   : Y = acc + bias[n] + rowbias[grp(m)][n] stored to C; per-128-row block
  *               column partials {mean, M2} of p (p = Y, or relu(Y) if stat_relu) into
- *               stat_ws[blk][2][N]; if pool_ws: per block column {max,argmax,min,argmin}
+ *               stat_ws[2][N][blk] (one column's block partials contiguous); if pool_ws: per block column {max,argmax,min,argmin}
  *               of Y into pool_ws[blk][4][N] (group_rows multiple of 128)
  *   EPI_BNBWD : dh = acc (+ pool_grad[g][n] where pool_idx[g][n] == m) (+ gadd[m][n]); with
  *               the previous layer's (Y, mean, invstd, scale, shift): ENC g = dh*(Y*scale+shift > 0),
@@ -195,13 +195,13 @@ typedef struct UredGemmDesc {
     const float* rowbias; int ldr;              /* [G][ldr] or NULL */
     const int* gidx; int group_rows;            /* row -> group: gidx[m] or m / group_rows */
     int stat_relu;
-    float* stat_ws;                             /* [ceil(M/128)][2][N] */
+    float* stat_ws;                             /* [2][N][ceil(M/128)] */
     float* pool_ws;                             /* [ceil(M/128)][4][N] or NULL */
     const float* Yp; int ldy;                   /* EPI_BNBWD: previous layer's raw output */
     const float* bn_mean; const float* bn_invstd; const float* bn_scale; const float* bn_shift;
     int bwd_res;                                /* URED_ACT_ENC / URED_ACT_RES / URED_ACT_BN */
     const int* pool_idx; const float* pool_grad; int pool_group_rows;
-    float* bwd_ws;                              /* [ceil(M/128)][2][N] */
+    float* bwd_ws;                              /* [2][N][ceil(M/128)] */
     int splits;                                 /* EPI_SPLITK: gridDim.z (k-range per split = ceil(K/splits/32)*32) */
     const float* gadd; int ldg;                 /* EPI_BNBWD: optional extra gradient, dh += gadd[m*ldg+n] */
 } UredGemmDesc;

@@ -31,12 +31,13 @@ def test_fwd_small_stats(K, dev, M, N, Kd, relu):
     ref = X.double() @ W.double().t() + b.double()
     assert (Y.double() - ref).abs().max().item() <= 1e-5 * (1 + ref.abs().max().item())
     p = ref.clamp_min(0) if relu else ref
+    wv = ws.view(2, N, _blocks(M))              # partial layout [2][N][blocks] (include/ured_hip.h)
     for blk in range(_blocks(M)):
         rows = p[blk * 128:(blk + 1) * 128]
         mu = rows.mean(0)
         m2 = ((rows - mu) ** 2).sum(0)
-        assert torch.allclose(ws[blk, 0].double(), mu, rtol=1e-5, atol=1e-5)
-        assert torch.allclose(ws[blk, 1].double(), m2, rtol=1e-4, atol=1e-4)
+        assert torch.allclose(wv[0, :, blk].double(), mu, rtol=1e-5, atol=1e-5)
+        assert torch.allclose(wv[1, :, blk].double(), m2, rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("M,N,Kd,mode,gadd", [(32768, 32, 3, 1, False), (1000, 64, 3, 0, True), (300, 256, 4, 2, False),
@@ -69,7 +70,8 @@ def test_dgrad_small_bnbwd(K, dev, M, N, Kd, mode, gadd):
         mask = y * scale.double() + shift.double() > 0
         gr, xh = torch.where(mask, dh, torch.zeros_like(dh)), (y - mean.double()) * invstd.double()
     assert (G.double() - gr).abs().max().item() <= 1e-5 * (1 + gr.abs().max().item())
+    wv = ws.view(2, N, _blocks(M))              # partial layout [2][N][blocks] (include/ured_hip.h)
     for blk in range(_blocks(M)):
         sl = slice(blk * 128, (blk + 1) * 128)
-        assert torch.allclose(ws[blk, 0].double(), gr[sl].sum(0), rtol=1e-4, atol=1e-4)
-        assert torch.allclose(ws[blk, 1].double(), (gr[sl] * xh[sl]).sum(0), rtol=1e-4, atol=1e-4)
+        assert torch.allclose(wv[0, :, blk].double(), gr[sl].sum(0), rtol=1e-4, atol=1e-4)
+        assert torch.allclose(wv[1, :, blk].double(), (gr[sl] * xh[sl]).sum(0), rtol=1e-4, atol=1e-4)
