@@ -40,7 +40,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 3
+#define URED_ABI_VERSION 4   /* 4: BN partial workspaces laid out [2][N][blocks]; ured_part_rows_bwd */
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
