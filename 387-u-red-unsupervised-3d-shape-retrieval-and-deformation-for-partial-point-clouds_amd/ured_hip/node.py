@@ -251,14 +251,13 @@ class NodeLinearFn(Function):
         M = x.shape[0]
         y = torch.empty(M, W.shape[0], device=x.device)
         linear(x, W, y, bias=b, R=R)
-        ctx.save_for_backward(x, W)
+        ctx.save_for_backward(x, W, b)
         ctx.has_b, ctx.has_r = b is not None, R is not None
-        ctx.b = b if (b is not None and b.is_leaf) else None    # a parameter: grad_buffer target
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x, W = ctx.saved_tensors
+        x, W, b = ctx.saved_tensors
         g = g.contiguous()
         dx = dW = db = None
         jobs = []
@@ -270,7 +269,7 @@ class NodeLinearFn(Function):
             dW, accW = grad_slot(W)
             jobs.append(wgrad_desc(g, x, dW, accumulate=accW))
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db, accb = grad_slot(ctx.b) if ctx.b is not None else (torch.empty(g.shape[1], device=g.device), False)
+            db, accb = grad_slot(b)
             jobs.append(colsum_desc(g, db, accumulate=accb))
         if jobs:
             launch(*jobs)
@@ -421,18 +420,16 @@ class NodeFFNFn(Function):
         out = torch.empty(M, W2.shape[0], device=dev)
         linear(act, W2, out, bias=b2, R=R)
         ctx.spec = spec
-        ctx.bparams = (b1, beta, b2)
-        ctx.save_for_backward(x, msg, W1, gamma, W2, Y1, act, mean, invstd)
+        ctx.save_for_backward(x, msg, W1, gamma, W2, Y1, act, mean, invstd, b1, beta, b2)
         return out
 
     @staticmethod
     def backward(ctx, g):
         bnm, off, training = ctx.spec
-        x, msg, W1, gamma, W2, Y1, act, mean, invstd = ctx.saved_tensors
+        x, msg, W1, gamma, W2, Y1, act, mean, invstd, b1, beta, b2 = ctx.saved_tensors
         g = g.contiguous()
         M, C = x.shape
         dev = x.device
-        b1, beta, b2 = ctx.bparams
         dact = torch.empty(act.shape, device=dev)
         (dW2, aW2), (db2, ab2) = grad_slot(W2), grad_slot(b2)
         launch(dgrad_desc(g, W2, dact), wgrad_desc(g, act, dW2, accumulate=aW2), colsum_desc(g, db2, accumulate=ab2))
@@ -478,18 +475,16 @@ class ParamDecoderFn(Function):
         out = torch.empty(BP, W2.shape[0], device=dev)
         linear(h, W2, out, bias=b2)
         ctx.P = P
-        ctx.bparams = (b1, b2)
-        ctx.save_for_backward(glob, parts, W1, W2, h)
+        ctx.save_for_backward(glob, parts, W1, W2, h, b1, b2)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        glob, parts, W1, W2, h = ctx.saved_tensors
+        glob, parts, W1, W2, h, b1, b2 = ctx.saved_tensors
         P = ctx.P
         B, Cg = glob.shape
         g = g.contiguous()
         dev = g.device
-        b1, b2 = ctx.bparams
         dW2 = grad_buffer(W2)
         db2 = grad_buffer(b2)
         dh = torch.empty(h.shape, device=dev)
