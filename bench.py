@@ -34,12 +34,12 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X fp32 (vector = matrix) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARY = "r2n_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
+PMC_SUMMARY = "r2o_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
 # rocprofv3 --kernel-trace --stats of the headline command (tools/prof_step.sh), restricted to its timed
 # steps: the dominant kernel's average duration there is what roofline.achieved / frac are computed from
-PROF_STATS = "r2n_step_kernel_stats.csv"
-CLOCK_SUMMARY = "r2n_clock_summary.json"   # GRBM_GUI_ACTIVE pass (tools/gpu_clock_sq.sh): clock held per kernel
-SQ_SUMMARY = "r2n_sq_summary.json"         # SQ pass (tools/gpu_clock_sq.sh): MFMA-busy cycles per kernel
+PROF_STATS = "r2o_step_kernel_stats.csv"
+CLOCK_SUMMARY = "r2o_clock_summary.json"   # GRBM_GUI_ACTIVE pass (tools/gpu_clock_sq.sh): clock held per kernel
+SQ_SUMMARY = "r2o_sq_summary.json"         # SQ pass (tools/gpu_clock_sq.sh): MFMA-busy cycles per kernel
 NOMINAL_GHZ = 2.4
 
 
@@ -411,9 +411,12 @@ def main():
     ap.add_argument("--no-breakdown", action="store_true")
     ap.add_argument("--breakdown-steps", type=int, default=3, help="eager steps timed per GEMM launch after the run")
     ap.add_argument("--shapes-out", default=None, help="write the per-shape GEMM breakdown (JSON) here")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the step as HIP graphs (engine/graph.py; N=1 unless --graph-dp). Measured "
-                         "equal to eager once the step has no host syncs, so eager is the default")
+    ap.add_argument("--eager", action="store_true",
+                    help="issue the step eagerly (Python + ctypes launches, ~700 per step) instead of replaying it "
+                         "as HIP graphs. Graph replay (engine/graph.py, bitwise equal to eager) is the default at "
+                         "N=1: the GPU-side step is ~16 ms, and on a slow host the eager launch stream cannot keep "
+                         "up (51 vs 63 it/s measured on one box); N > 1 replays only with --graph-dp")
+    ap.add_argument("--graph", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old commands
     ap.add_argument("--graph-dp", action="store_true", help="HIP-graph replay also when N > 1")
     ap.add_argument("--graph-bucket", type=int, default=1,
                     help="graph mode: pad the distinct-source-part count to a multiple of this (one graph per count)")
@@ -459,7 +462,7 @@ def main():
     from dataset import synthetic
 
     cfg = workload_cfg(args)
-    use_graph = args.graph and (world == 1 or args.graph_dp)
+    use_graph = not args.eager and (world == 1 or args.graph_dp)
     cfg["cuda_graph"] = use_graph
     cfg["stream_overlap"] = args.overlap
     cfg["deform_overlap"] = args.deform_overlap
@@ -476,6 +479,13 @@ def main():
     else:
         step = eager
 
+    b0 = None
+    if use_graph:
+        # the dominant GEMM variant's launches / FLOPs / bytes per step (for the roofline) from one
+        # eager step with an event pair per GEMM launch, before the graphs are captured
+        with GemmTimer() as gt0:
+            eager.step(batches[0])
+        b0 = gt0.summary()
     for i in range(args.warmup):
         step.step(batches[i % 4])
     # one more untimed step with an event pair per GEMM launch picks the dominant kernel
@@ -562,16 +572,18 @@ def main():
     iters_per_s = args.steps / elapsed
     roofline = None
     extra = {}
-    if breakdown or dom is not None:
+    if breakdown or dom is not None or b0:
         if dom is not None:     # measured inside the timed region
             dom_key = dom.key
             d = dom.summary()
             timing = "HIP events around each launch of this kernel inside the timed region"
             lps = d["launches"] / args.steps
-        else:
-            dom_key = max(breakdown, key=lambda k: breakdown[k]["ms"])
-            d = breakdown[dom_key]
-            timing = "HIP events around each launch in separate eager steps after the timed region"
+        else:                   # graph replay: per-launch events from eager steps outside it
+            src = breakdown if breakdown else b0
+            dom_key = max(src, key=lambda k: src[k]["ms"])
+            d = src[dom_key]
+            timing = ("HIP events around each launch in separate eager steps after the timed region" if breakdown
+                      else "HIP events around each launch in one eager step before the timed region")
             lps = d["launches"]
         avg_ms = d["ms"] / d["launches"]
         flop_per_launch = d["flop"] / d["launches"]

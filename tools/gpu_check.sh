@@ -1,4 +1,4 @@
-# GPU-box check: gpu tests, smoke, bench (eager + graph). Stops at the first failure.
+# GPU-box check: gpu tests, smoke, bench (graph replay, the default, + eager). Stops at the first failure.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
@@ -9,5 +9,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/smoke.log
 timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
-timeout -k 10 300 python bench.py --graph --no-cpu-baseline --no-all-slots-rate > gpurun_out/bench_graph.log 2>&1 || { echo "bench graph failed"; tail -30 gpurun_out/bench_graph.log; exit 1; }
-tail -1 gpurun_out/bench_graph.log
+timeout -k 10 300 python bench.py --eager --no-cpu-baseline --no-all-slots-rate > gpurun_out/bench_eager.log 2>&1 || { echo "bench eager failed"; tail -30 gpurun_out/bench_eager.log; exit 1; }
+tail -1 gpurun_out/bench_eager.log

@@ -15,9 +15,9 @@ tail -1 $R/gpurun_out/${T}_stats.log
 timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/${T}_trace -o step --output-format csv -- python3 $R/bench.py $B > $R/gpurun_out/${T}_trace.log 2>&1 || { echo "trace run failed rc=$?"; tail -20 $R/gpurun_out/${T}_trace.log; exit 1; }
 tail -1 $R/gpurun_out/${T}_trace.log
 cd $R
-# all launches, and only the timed steps (bench: 3 warmup + 1 GEMM-timer step + K timed steps)
+# all launches, and only the timed steps (bench default, graph replay: 1 GEMM-timer eager step + 4 warmup steps (eager + capture) + K replayed steps)
 python3 tools/trace_stats.py gpurun_out/${T}_trace gpurun_out/${T}_trace_stats.csv --top 60 > gpurun_out/${T}_trace_top.txt
-python3 tools/trace_stats.py gpurun_out/${T}_trace gpurun_out/${T}_trace_timed_stats.csv --tail $K/$((K + 4)) --top 60 > gpurun_out/${T}_trace_timed_top.txt
-python3 tools/trace_stats.py gpurun_out/${T}_stats gpurun_out/${T}_stats_timed_stats.csv --tail $K/$((K + 4)) --top 5 > /dev/null
+python3 tools/trace_stats.py gpurun_out/${T}_trace gpurun_out/${T}_trace_timed_stats.csv --tail $K/$((K + 5)) --top 60 > gpurun_out/${T}_trace_timed_top.txt
+python3 tools/trace_stats.py gpurun_out/${T}_stats gpurun_out/${T}_stats_timed_stats.csv --tail $K/$((K + 5)) --top 5 > /dev/null
 find gpurun_out/${T}_stats gpurun_out/${T}_trace -name "*kernel_trace.csv" -delete
 head -30 gpurun_out/${T}_trace_top.txt
