@@ -110,9 +110,24 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+# the raw handle of torch's current stream (honours torch.cuda.stream contexts and graph capture)
+# without building a Stream object: ~0.3 us instead of ~7 us per launch, which matters for the
+# eager step's host issue rate (~1100 launches through here per config-2 step)
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_of(t):
     """The current torch stream on t's device, as a hipStream_t handle."""
+    if _RAW_STREAM is not None and t.device.index is not None:
+        return ctypes.c_void_p(_RAW_STREAM(t.device.index))
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def current_stream():
+    """The current torch stream on the current device, as a hipStream_t handle."""
+    if _RAW_STREAM is not None:
+        return ctypes.c_void_p(_RAW_STREAM(torch.cuda.current_device()))
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
 def require_device(*tensors):

@@ -119,7 +119,7 @@ def colsum_desc(g, out, accumulate=False):
 
 def launch(*descs):
     """Run independent node GEMMs (up to 4 per launch) on the current stream."""
-    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    stream = _lib.current_stream()
     for i in range(0, len(descs), MAX_JOBS):
         part = descs[i:i + MAX_JOBS]
         arr = (ctypes.POINTER(NodeGemmDesc) * len(part))(*[ctypes.pointer(d) for d in part])

@@ -29,6 +29,7 @@ def _zeros_empty(*a, **k):
 def stub():
     _lib.call = lambda name, *a: None
     _lib.stream_of = lambda t: None
+    _lib.current_stream = lambda: None
     _lib.require_device = lambda *t: None
     import ured_hip.mlp as mlp
     mlp._nbt = lambda bnm: bnm.num_batches_tracked
