@@ -73,7 +73,11 @@ def compute_cm_loss_pair(source_p, source_p2, target_p, target_part, mask, np_pe
                         _doubled(parts, B, N, P), torch.cat([mask, mask]), batch_reduction=None,
                         np_per_part=np_per_part, return_idx=return_idx)
     full, part = r[0], r[1]
-    res = (full[:B].mean(), part[:B].mean()), (full[B:].mean(), part[B:].mean())
+    # per-half means as one op each, split by unbind (its backward is one stack; slicing the
+    # halves would cost a zero-fill + copy per slice and an add)
+    f0, f1 = full.view(2, B).mean(1).unbind(0)
+    p0, p1 = part.view(2, B).mean(1).unbind(0)
+    res = (f0, p0), (f1, p1)
     return res + (r[2][:B],) if return_idx else res
 
 
@@ -108,7 +112,10 @@ def compute_cm_loss(source_p, target_p, target_part=None, mask=None, batch_reduc
     psegs = torch.stack([a_off, a_len, b_off, b_len], -1).view(B * P, 4).int()
     pa, _, pb, _ = nn_segments(src, parts.x_sorted.contiguous(), psegs, np_per_part, N, 3)
     nchunk = min(S, P * np_per_part) // np_per_part
-    cost1 = pa.view(B, S)[:, :nchunk * np_per_part].reshape(B, nchunk, np_per_part).mean(-1)
+    pa2 = pa.view(B, S)
+    if nchunk * np_per_part != S:      # (a full-width slice would still cost a zero-fill + copy backward)
+        pa2 = pa2[:, :nchunk * np_per_part]
+    cost1 = pa2.reshape(B, nchunk, np_per_part).mean(-1)
     if nchunk < P:
         cost1 = torch.cat([cost1, cost1.new_zeros(B, P - nchunk)], 1)
     cost2 = segment_sum(pb.view(-1, 1), parts.off, parts.gid).view(B, P) / parts.counts.clamp(min=1).float()
