@@ -40,6 +40,7 @@ def all_gather_batch(tensors, differentiable=False):
 
 
 LOGIT_SCALE = math.log(1 / 0.07)
+_SCALE32 = float(torch.tensor(LOGIT_SCALE, dtype=torch.float32).exp())
 
 
 def compute_contrast_loss_loss(tgt_part_f, src_f, src_labels, differentiable_gather=False):
@@ -47,12 +48,11 @@ def compute_contrast_loss_loss(tgt_part_f, src_f, src_labels, differentiable_gat
     t = tgt_part_f.reshape(bs * num_part, -1)
     s = src_f.reshape(bs * num_part, -1)
     n = bs * num_part
-    labels = n * get_rank() + torch.arange(n, device=t.device)
-    labels = torch.where(src_labels.reshape(n).to(t.device) == -1, torch.full_like(labels, -1), labels)
+    labels = (n * get_rank() + torch.arange(n, device=t.device)).masked_fill_(src_labels.reshape(n).to(t.device) == -1, -1)
     t_e = F.normalize(t, dim=-1, p=2)
     s_e = F.normalize(s, dim=-1, p=2)
     _, s_all = all_gather_batch([t_e, s_e], differentiable=differentiable_gather)
-    scale = torch.full((), LOGIT_SCALE, device=t.device).exp()   # a fill kernel: graph-capturable (no H2D copy)
+    scale = _SCALE32                    # exp(logit scale) rounded to fp32 once, as the fp32 tensor exp would
     if t_e.is_cuda:
         # logits t_e s_all^T on the node GEMM (csrc/node.hip): forward and both backward GEMMs
         from ured_hip.node import node_linear
