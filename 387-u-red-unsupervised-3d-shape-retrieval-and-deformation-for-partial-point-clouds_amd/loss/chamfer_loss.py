@@ -101,14 +101,14 @@ def compute_cm_loss(source_p, target_p, target_part=None, mask=None, batch_reduc
     da, _, db, ib = nn_segments(src, target_p.contiguous(), segs, S, N, 3)
     n_valid = (k * np_per_part).clamp(min=1).float()
     full = da.view(B, S).sum(1) / n_valid + db.view(B, N).mean(1)
-    full = torch.where(k > 0, full, torch.full_like(full, float("nan")))
+    full = full.masked_fill(k == 0, float("nan"))
     # part family: part slot i of sample b <-> points of its i-th part (sorted by label)
     slot = torch.arange(P, device=dev)
     valid = slot.unsqueeze(0) < k.unsqueeze(1)
     a_off = (torch.arange(B, device=dev) * S).unsqueeze(1) + slot.unsqueeze(0) * np_per_part
-    a_len = torch.where(valid, torch.full_like(a_off, np_per_part), torch.zeros_like(a_off))
+    a_len = valid.long() * np_per_part
     b_off = parts.off[:-1].view(B, P).long()
-    b_len = torch.where(valid, parts.counts, torch.zeros_like(parts.counts))
+    b_len = parts.counts * valid
     psegs = torch.stack([a_off, a_len, b_off, b_len], -1).view(B * P, 4).int()
     pa, _, pb, _ = nn_segments(src, parts.x_sorted.contiguous(), psegs, np_per_part, N, 3)
     nchunk = min(S, P * np_per_part) // np_per_part
