@@ -38,11 +38,13 @@ if os.path.dirname(_HERE) not in sys.path:
     sys.path.insert(0, os.path.dirname(_HERE))
 
 from dataset import synthetic  # noqa: E402
+from engine.config import check_config  # noqa: E402
 from dataset.dataset_utils import get_shape, get_source_info, get_source_points, get_symmetric  # noqa: E402
 from loss.basic_consistency_loss import compute_pc_consistency, compute_pc_consistency_weighted  # noqa: E402
 from loss.basic_loss import residual_retrieval_loss  # noqa: E402
 from loss.chamfer_loss import compute_cm_loss, compute_cm_loss_pair  # noqa: E402
 from loss.contrast_loss import compute_contrast_loss_loss  # noqa: E402
+from loss.regularization_loss import regularization_param  # noqa: E402
 from network.deformation_net import DeformNet_MatchingNet as DM_decoder  # noqa: E402
 from network.deformation_net import re_residual_net  # noqa: E402
 from network.simple_encoder import TargetEncoder as simple_encoder  # noqa: E402
@@ -121,6 +123,7 @@ class TrainStep:
         self.models, self.optimizer, self.scheduler = get_models(cfg, device)
         self.np_per_part = db.points.shape[1]
         dev = torch.device(device or cfg["device"])
+        self._zflip = torch.tensor([1.0, 1.0, -1.0], device=dev)
         self.side_stream = (torch.cuda.Stream(device=dev)
                             if dev.type == "cuda" and cfg.get("stream_overlap", False) else None)
         self.deform_stream = (torch.cuda.Stream(device=dev)
@@ -157,6 +160,9 @@ class TrainStep:
         out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
         contrast_labels = torch.where(src_labels >= 0, torch.ones_like(src_labels), src_labels)
         loss = out.new_zeros(())
+        if cfg.get("use_param_loss", 0.0) > 0.0:     # engine/train.py:281-283 (first term, as there)
+            T["param_loss"] = regularization_param(params_full, mask_part)
+            loss = loss + T["param_loss"] * cfg["use_param_loss"]
         pair = cfg["use_chamfer_loss"] > 0.0 and cfg["use_symmetry_loss"] > 0.0
         knn_idx = None
         if pair:        # both chamfer families of out and of its mirror image in one launch each
@@ -183,6 +189,10 @@ class TrainStep:
         cfg, M = self.cfg, self.models
         P = cfg["MAX_NUM_PARTS"]
         x = batch["x"]
+        if cfg.get("complementme", False):
+            # engine/train.py:192-194: ComplementMe targets are z-flipped (the reference negates the
+            # batch tensor in place; the batch here may be replayed, so the flip is out of place)
+            x = x * self._zflip
         B, N, _ = x.shape
         src_labels = batch["src_labels"]
         mats, _, src_sem_idx = get_source_info(src_labels, self.db)
@@ -358,6 +368,9 @@ class PseudoLabelLoader:
         P = cfg["MAX_NUM_PARTS"]
         T = int(cfg.get("num_targets", 128))
         self.bs = cfg["batch_size"]
+        if T < self.bs:
+            raise ValueError(f"num_targets ({T}) < batch_size ({self.bs}): every epoch would be empty "
+                             "(the reference's DataLoader drops the last partial batch)")
         t = synthetic.make_batch(T, cfg.get("num_points", 2048), db.num_sources, max_parts=P,
                                  parts=cfg.get("parts", 4), seed=seed * 7777 + 17)
         self.targets = t
@@ -372,7 +385,7 @@ class PseudoLabelLoader:
         src = np.stack([normalize_pts(p) for p in db.points.cpu().numpy()])
         gen = PairGenerator(torch.from_numpy(src).to(device))
         table = gen.cross(torch.from_numpy(np.concatenate(clouds)))          # [3, parts, NS]
-        self.table = PseudoLabelTable(table[2], part_sem, db.sem, np.asarray(dist_src)[2],
+        self.table = PseudoLabelTable(table[2], part_sem, db.sem, np.asarray(dist_src),
                                       alpha=cfg.get("filter_threshold", 2e-2), cl_k=cfg.get("cl_k", 40),
                                       device=device)
         self.part_rows = rows
@@ -462,6 +475,7 @@ def init_distributed(cfg):
 
 
 def main(cfg):
+    check_config(cfg, "train")
     rank, world, device = init_distributed(cfg)
     db, dist_src = load_sources(cfg, device)
     if world > 1:

@@ -15,6 +15,8 @@ dicts, following (reference root = the U-RED repo):
   residual_retrieval_loss        loss/basic_loss.py:249-265
   consistency losses             loss/basic_consistency_loss.py:4-22
   contrast loss                  loss/contrast_loss.py:61-102
+  regularization_param           loss/regularization_loss.py:49-53 (cfg["use_param_loss"] > 0)
+  complementme z-flip            engine/train.py:192-194 (cfg["complementme"])
   loss assembly / optimiser      engine/train.py:196-345, train_utils/optimizer_dm.py:68-104
 
 Pinned against reference-generated golden vectors (tests/golden/make_golden.py).
@@ -352,6 +354,12 @@ def pc_consistency_weighted(a, b, mask):
     return (per * mask).sum() / mask.sum()
 
 
+def regularization_param(params_full, mask_part):
+    """loss/regularization_loss.py:49-53: boolean-indexed rows, then the mean L2 norm."""
+    m = mask_part.reshape(-1).bool()
+    return torch.norm(params_full.reshape(-1, 6)[m], p=2, dim=-1).mean()
+
+
 def contrast_loss(tgt_part_f, src_f, src_labels, rank=0, gathered_src=None):
     B, Pn = src_f.shape[0], src_f.shape[1]
     t = F.normalize(tgt_part_f.reshape(B * Pn, -1), dim=-1, p=2)
@@ -385,6 +393,9 @@ def train_forward(params, batch, cfg, training=True, epoch=0):
     src_sem_f = emb[batch["src_sem"][src_idx]]
     tgt_sem_f = emb[batch["tgt_sem"]]
     x = batch["x"]
+    if cfg.get("complementme", False):
+        x = x.clone()
+        x[:, :, 2] = -x[:, :, 2]
     B = x.shape[0]
 
     codes, src_pp = target_encoder(params["src_encoder_all"], src_pts, src_sem_f, True, training)
@@ -404,6 +415,9 @@ def train_forward(params, batch, cfg, training=True, epoch=0):
     out = get_shape(mats, prm, param_def, cfg["alpha"]).reshape(B, -1, 3)
 
     T = OrderedDict()
+    use_param = cfg.get("use_param_loss", 0.0) > 0.0
+    if use_param:
+        T["param_loss"] = regularization_param(prm, mask)
     T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask)
     T["contrast_loss"] = contrast_loss(part_f, codes, batch["src_labels"])
     T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(get_symmetric(out), x, part_x, mask)
@@ -411,7 +425,8 @@ def train_forward(params, batch, cfg, training=True, epoch=0):
         T["re_reg_loss_full"], T["reg_loss_full"] = residual_retrieval_loss(x, out.detach(), re_res, mask)
     T["recon_loss_full"] = pc_consistency(recon_full, x)
     T["recon_loss_src"] = pc_consistency_weighted(recon_src, src_pts, mask)
-    loss = (T["cd_loss_full"] * cfg["use_chamfer_loss"] + T["cd_loss_part"] * cfg["use_chamfer_part_loss"]
+    loss = T["param_loss"] * cfg["use_param_loss"] if use_param else 0.0
+    loss = (loss + T["cd_loss_full"] * cfg["use_chamfer_loss"] + T["cd_loss_part"] * cfg["use_chamfer_part_loss"]
             + T["contrast_loss"] * cfg["use_contrast_loss"] + T["ref_cd_loss_full"] * cfg["use_symmetry_loss"])
     if "re_reg_loss_full" in T:
         loss = loss + T["re_reg_loss_full"] * cfg["use_residuals_reg"] + T["reg_loss_full"] * cfg["use_residuals_reg"] * 0.01

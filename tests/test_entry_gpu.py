@@ -32,13 +32,13 @@ def test_pseudo_label_loader_matches_get_labels(dev, tmp_path):
     from train_utils.load_sources import load_sources
     cfg = _cfg(tmp_path, filter_threshold=1.0)
     db, dist_src = load_sources(cfg, dev)
-    assert dist_src.shape == (3, 48, 48) and np.allclose(dist_src, dist_src.transpose(0, 2, 1))
-    assert (dist_src[2] > 0).mean() > 0.9
+    assert dist_src.shape == (48, 48) and np.allclose(dist_src, dist_src.T)   # the cd_m plane
+    assert (dist_src > 0).mean() > 0.9
     ld = PseudoLabelLoader(cfg, db, dev, dist_src, seed=3)
     rows = ld.part_rows
     lists = [[int(r) for r in row if r >= 0] for row in rows]
     exp = ref.get_labels(lists, ld.table.cd_m.cpu().numpy(), ld.table.part_sem.cpu().numpy(), db.sem.cpu().numpy(),
-                         dist_src[2], cfg["filter_threshold"], cfg["cl_k"], cfg["MAX_NUM_PARTS"])
+                         dist_src, cfg["filter_threshold"], cfg["cl_k"], cfg["MAX_NUM_PARTS"])
     np.testing.assert_array_equal(ld.labels, exp)
     assert (exp[:, :3] >= 0).any()
     batches = list(ld)

@@ -13,11 +13,12 @@ Oracle: oracle/ured_ref.py in float64 on the host (weights and inputs; its chamf
 the fp32 C contract of oracle/nn_oracle.c), ~30-50 s per configuration on 16 threads; one
 oracle run serves both source-encoding modes of a configuration.
 
-Tolerances (written here, same rules as tests/test_train_step_gpu.py):
-  * every loss term within 2e-5 relative (north star: loss within 1e-5; the total is ~1e2);
+Tolerances (tests/step_parity.py, same rules as tests/test_train_step_gpu.py):
+  * every loss term within 1e-5 relative (SURVEY §8(d)); the deviations are printed;
   * the deformed shape within 1e-4 of its largest coordinate;
-  * per-parameter gradient norms within 5e-3 relative (max-pool argmax near-ties flip between
-    summation orders), the BN-fed conv biases (true gradient exactly 0) at noise level;
+  * every parameter gradient tensor compared whole: ||g - g_ref|| / ||g_ref|| <= 1e-3 and the
+    elementwise max deviation within 2e-3 of the tensor's largest entry; the exactly-zero true
+    gradients (BN-fed conv biases, attention key biases) at noise level;
   * NN distances and indices of the step's own chamfer families bit-exact against the C oracle
     run on the same (GPU-produced) inputs and segment tables;
   * retrieval indices bit-exact except where the oracle's top-2 cosine gap is < 1e-6 (SURVEY
@@ -30,6 +31,7 @@ import numpy as np
 import pytest
 import torch
 
+import step_parity
 from conftest import PKG_DIR
 from oracle import nn_ref, ured_ref
 
@@ -37,8 +39,6 @@ pytestmark = pytest.mark.gpu
 
 TERMS = ("cd_loss_full", "cd_loss_part", "contrast_loss", "ref_cd_loss_full", "ref_cd_loss_part",
          "re_reg_loss_full", "reg_loss_full", "recon_loss_full", "recon_loss_src", "all_loss")
-BN_FED_BIAS = ("mlp1.0.bias", "mlp1.3.bias", "mlp2.0.bias", "mlp2.3.bias", "mlp2.6.bias", "fuse_sem.0.bias",
-               "per_point_out.0.bias", "fc.0.bias")
 NS = 512
 _ORACLE = {}
 
@@ -82,19 +82,17 @@ def _oracle_batch(db_np, bt, dtype=torch.float64):
 
 
 def _oracle_step(key, cfg, db_np, bt):
-    """float64 oracle forward + backward, cached per configuration: (terms, out, grad norms)."""
+    """float64 oracle forward + backward, cached per configuration: (terms, out, gradients)."""
     if key not in _ORACLE:
         _threads()
         _, P64 = _params64(cfg, seed=7)
         loss, R = ured_ref.train_forward(P64, _oracle_batch(db_np, bt), cfg)
         loss.backward()
         terms = {k: float(R[k]) for k in TERMS}
-        gn = {}
-        for mod, sd in P64.items():
-            for k, v in sd.items():
-                if torch.is_tensor(v) and v.requires_grad:
-                    gn[(mod, k)] = None if v.grad is None else float(v.grad.norm())
-        _ORACLE[key] = (terms, R["_out"].detach().float(), gn)
+        grads = {(mod, k): (None if v.grad is None else v.grad.detach().clone())
+                 for mod, sd in P64.items() if mod != "embedding_layer"
+                 for k, v in sd.items() if torch.is_tensor(v) and v.requires_grad}
+        _ORACLE[key] = (terms, R["_out"].detach().float(), grads)
         del loss, R, P64
     return _ORACLE[key]
 
@@ -125,29 +123,13 @@ def _check_step(dev, B, N, parts, unique):
     got_terms = {k: float(T[k]) for k in TERMS}
     out = T["_out"].detach()
     loss.backward()
-    rterms, rout, rgn = _oracle_step((B, N, parts), cfg, db_np, bt)
-    for k in TERMS:
-        assert abs(got_terms[k] - rterms[k]) <= 2e-5 * abs(rterms[k]) + 1e-7, f"{k}: {got_terms[k]} vs {rterms[k]}"
+    rterms, rout, rgrads = _oracle_step((B, N, parts), cfg, db_np, bt)
+    label = f"B={B} N={N} k={parts} unique={unique}"
+    step_parity.check_loss_terms(got_terms, rterms, label)
     o = out.cpu()
     assert (o - rout).abs().max().item() <= 1e-4 * rout.abs().max().item()
-    n = 0
-    for mod in ("target_encoder_full", "param_decoder_full", "re_residual_net_full", "recon_decoder_full",
-                "src_encoder_all", "recon_decoder_src"):
-        params = dict(ts.models[mod].named_parameters())
-        for k, p in params.items():
-            rn = rgn.get((mod, k))
-            if rn is None:
-                assert p.grad is None, f"{mod}.{k} should get no gradient"
-                continue
-            assert p.grad is not None, f"{mod}.{k}"
-            gn = p.grad.norm().item()
-            if k in BN_FED_BIAS:
-                wn = params[k.replace(".bias", ".weight")].grad.norm().item()
-                assert gn <= 1e-2 * wn + 1e-4 and rn <= 1e-2 * wn + 1e-4, f"{mod}.{k}: {gn} {rn} vs |dW| {wn}"
-                continue
-            assert abs(gn - rn) <= 5e-3 * rn + 1e-4, f"{mod}.{k}: |g| {gn} vs {rn}"
-            n += 1
-    assert n > 150
+    n, _ = step_parity.check_grads(ts.models, rgrads, label)
+    assert n >= 145
     _check_step_nn(out, batch, cfg)
     return got_terms
 
