@@ -51,7 +51,7 @@ from network.simple_encoder import TargetEncoder as simple_encoder  # noqa: E402
 from train_utils.load_sources import load_sources  # noqa: E402
 from train_utils.optimizer_dm import define_optimizer_dm_re_recon  # noqa: E402
 from ured_hip.kernels import RowWeights  # noqa: E402
-from ured_hip.ops import UniqueRows, build_parts, part_aabb, part_rows  # noqa: E402
+from ured_hip.ops import UniqueRows, build_parts, part_aabb, part_rows, upload  # noqa: E402
 
 MODULE_NAMES = ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "re_residual_net_full",
                 "src_encoder_all", "recon_decoder_src", "embedding_layer")
@@ -320,13 +320,12 @@ class TrainStep:
 
 
 def batch_to_device(b, device, num_sources=None, bucket=None):
-    """Host batch -> device tensors. With num_sources (the source DB size) the distinct source
+    """Host batch -> device tensors (pinned-memory staged, asynchronous on the current stream:
+    the reference's per-iteration .to(cfg["device"]) copies, engine/train.py:223-232). With num_sources (the source DB size) the distinct source
     parts of the batch are also computed here, on the host labels (UniqueRows; used by
     TrainStep unless cfg["unique_sources"] is False); `bucket` pads their count for HIP-graph
     replay (engine/graph.py keeps one graph per padded count)."""
-    out = {"x": torch.as_tensor(b["x"]).to(device), "labels": torch.as_tensor(b["labels"]).to(device),
-           "tgt_sem": torch.as_tensor(b["tgt_sem"]).to(device),
-           "src_labels": torch.as_tensor(b["src_labels"]).to(device)}
+    out = {k: upload(b[k], device) for k in ("x", "labels", "tgt_sem", "src_labels")}
     if num_sources is not None:
         out["src_unique"] = UniqueRows(b["src_labels"], num_sources, device, bucket=bucket)
     return out

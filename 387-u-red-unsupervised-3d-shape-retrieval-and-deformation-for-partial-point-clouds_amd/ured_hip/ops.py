@@ -198,6 +198,16 @@ class ExpandGroupsFn(Function):
         return gu.view(ctx.U, *g.shape[1:]), None, None, None
 
 
+def upload(a, device):
+    """Host array -> device tensor. To a GPU: staged through pinned memory (torch's caching host
+    allocator, which keeps the block until the copy has completed) and copied asynchronously on
+    the current stream, so a per-step batch upload does not stall the host."""
+    t = torch.as_tensor(a)
+    if torch.device(device).type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 class UniqueRows:
     """Distinct entries of a batch of source-part slots (engine/train.py:196-211: every slot
     whose label is -1 — and any repeated label — encodes the same source part).
@@ -224,11 +234,11 @@ class UniqueRows:
                 cnt = np.concatenate([cnt, np.zeros(pad, cnt.dtype)])
                 off = np.concatenate([off, np.full(pad, off[-1], np.int32)])
         self.U = int(uniq.shape[0])
-        self.uniq = torch.from_numpy(uniq).to(device)
-        self.inverse = torch.from_numpy(inv.reshape(-1).astype(np.int64)).to(device)
-        self.order = torch.from_numpy(order.astype(np.int64)).to(device)
-        self.off = torch.from_numpy(off).to(device)
-        self.w = torch.from_numpy(cnt.astype(np.float32)).to(device)
+        self.uniq = upload(uniq, device)
+        self.inverse = upload(inv.reshape(-1).astype(np.int64), device)
+        self.order = upload(order.astype(np.int64), device)
+        self.off = upload(off, device)
+        self.w = upload(cnt.astype(np.float32), device)
 
     FIELDS = ("uniq", "inverse", "order", "off", "w")
 

@@ -168,21 +168,25 @@ class GemmTimer:
         return dict(sorted(by.items(), key=lambda kv: -kv[1]["ms"]))
 
 
-def cpu_baseline(args, cfg_small_threads=16):
-    """The oracle (CPU restatement, torch fp32) timed on this host on a bounded sample."""
+def host_threads():
+    """The host cores this process may use: its CPU affinity, capped by OMP_NUM_THREADS when set
+    (the GPU box exports 16 = its CPU share; os.cpu_count() there is the whole machine's)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+def _oracle_step_rate(cfg, batch_size, points, parts, sources, warm=1, timed=3):
+    """1 warm-up + `timed` full oracle train steps (fwd + bwd + Adam, torch-CPU fp32) -> s/step."""
     from oracle import ured_ref
     from dataset import synthetic
-    threads = min(cfg_small_threads, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    cfg = workload_cfg(args)
     P = ured_ref.make_params(cfg, seed=0)
     for mod in P.values():
         for k, v in mod.items():
             if v.dtype.is_floating_point and "running" not in k:
                 v.requires_grad_(True)
-    ns = min(args.sources, 64)
-    db = synthetic.make_source_db(ns, seed=1)
-    bt = synthetic.make_batch(args.batch, args.points, ns, parts=args.parts, seed=0)
+    db = synthetic.make_source_db(sources, seed=1)
+    bt = synthetic.make_batch(batch_size, points, sources, parts=parts, seed=0)
     ob = {"src_points": torch.from_numpy(db["src_points"]), "src_mats": torch.from_numpy(db["src_mats"]),
           "src_sem": torch.from_numpy(db["src_sem"]), "src_index": torch.from_numpy(bt["src_index"]),
           "tgt_sem": torch.from_numpy(bt["tgt_sem"]), "x": torch.from_numpy(bt["x"]),
@@ -190,14 +194,53 @@ def cpu_baseline(args, cfg_small_threads=16):
           "src_labels": torch.from_numpy(np.where(bt["src_labels"] >= 0, 1, bt["src_labels"]))}
     params = [v for _, _, v in ured_ref.trainable(P)]
     opt = torch.optim.Adam(params, lr=1e-3, weight_decay=5e-4)
-    t0 = time.time()
-    loss, _ = ured_ref.train_forward(P, ob, cfg)
-    loss.backward()
-    opt.step()
-    dt = time.time() - t0
-    return {"value": 1.0 / dt, "unit": "iters/s", "cores": threads, "kind": "port",
-            "sample": f"1 full oracle train step (fwd+bwd+Adam) at the bench shape bs={args.batch} "
-                      f"N={args.points} on {threads} host threads, {dt:.1f} s"}
+    ts = []
+    for i in range(warm + timed):
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        loss, _ = ured_ref.train_forward(P, ob, cfg)
+        loss.backward()
+        opt.step()
+        ts.append(time.perf_counter() - t0)
+    return ts[warm:]
+
+
+def _distchamfer_rate(B=16, n=2048, m=2048, reps=3):
+    """The reference's Python chamfer (chamfer_python.distChamfer: float64 expansion matrix, min /
+    argmin both ways), restated in the oracle -> Gpair-dist/s at 16 x 2048 x 2048."""
+    from oracle import nn_ref
+    g = torch.Generator().manual_seed(0)
+    p1 = torch.rand(B, n, 3, generator=g)
+    p2 = torch.rand(B, m, 3, generator=g)
+    nn_ref.dist_chamfer(p1, p2)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        nn_ref.dist_chamfer(p1, p2)
+    t = (time.perf_counter() - t0) / reps
+    return B * n * m / t / 1e9, t
+
+
+def cpu_baseline(args):
+    """The oracle (the CPU restatement of the reference's step, torch-CPU fp32) timed on this
+    host, as BASELINE.md §2 plans: 1 warm-up + 3 timed full train steps at config 2 (the bench
+    shape, 512 sources) and at config 1 (bs 2, 512 points), and the reference's Python chamfer
+    (distChamfer) at 16 x 2048 x 2048 — all on host_threads() threads."""
+    threads = host_threads()
+    torch.set_num_threads(threads)
+    cfg = workload_cfg(args)
+    t2 = _oracle_step_rate(cfg, args.batch, args.points, args.parts, args.sources)
+    cfg1 = dict(cfg, batch_size=2)
+    t1 = _oracle_step_rate(cfg1, 2, 512, 4, args.sources)
+    gp, tch = _distchamfer_rate()
+    s2, s1 = sum(t2) / len(t2), sum(t1) / len(t1)
+    return {"value": round(1.0 / s2, 5), "unit": "iters/s", "cores": threads, "kind": "port",
+            "sample": f"oracle train step (fwd+bwd+Adam, torch-CPU fp32) at config 2 (bs={args.batch}, "
+                      f"N={args.points}, {args.sources} sources, {args.parts} parts): 1 warm-up + {len(t2)} timed "
+                      f"steps, {s2:.1f} s/step, on {threads} host threads",
+            "config1_iters_s": round(1.0 / s1, 4),
+            "config1_sample": f"config 1 (bs=2, N=512): 1 warm-up + {len(t1)} timed steps, {s1:.2f} s/step",
+            "distchamfer_gpair_s": round(gp, 4),
+            "distchamfer_sample": f"chamfer_python.distChamfer restated (float64 matrix), 16x2048x2048, {tch * 1e3:.0f} ms"}
 
 
 def chamfer_rate(dev, B=16, n=2048, m=2048, iters=20):
@@ -344,6 +387,46 @@ def pair_rate(dev, parts=512, pts=1024):
             "pairs_per_s": round(npairs / t, 1), "gpair_dist_s": round(npairs * pts * pts / t / 1e9, 1)}
 
 
+def loader_rate(step, cfg, db, dev, steps, world=1, rank=0, warm_epochs=2):
+    """The reference's per-iteration data path inside the timed loop (engine/train.py:190-232):
+    every step takes its batch from engine/train.py's PseudoLabelLoader — a seeded shuffle of a
+    fixed synthetic target set whose source labels are the reference's get_labels rule evaluated
+    on the device over a calc_dcd table (PseudoLabelTable) — builds the batch's distinct-source
+    tables on the host and uploads it from pinned host memory (asynchronous copies on the step's
+    stream), then runs the same step as the headline (graph replay at N=1). Warm-up: whole epochs,
+    so the graphs of the batch shapes an epoch produces are captured before timing."""
+    from engine.train import PseudoLabelLoader
+    from train_utils.load_sources import source_connectivity
+    dist_src = source_connectivity(db)[2]
+    lcfg = dict(cfg, num_targets=max(128, 8 * cfg["batch_size"]))
+    ld = PseudoLabelLoader(lcfg, db, dev, dist_src, seed=17 + rank)
+
+    def batches():
+        while True:
+            yield from ld
+    it = batches()
+    for _ in range(warm_epochs * len(ld)):
+        step.step(next(it))
+    graphs0 = len(getattr(step, "graphs", {}))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step.step(next(it))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    tt = torch.tensor([time.perf_counter() - t0], device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return {"iters_s": round(steps * world / float(tt.item()), 4), "steps": steps,
+            "graphs_captured_in_timed_steps": len(getattr(step, "graphs", {})) - graphs0,
+            "num_targets": lcfg["num_targets"],
+            "what": "each step: PseudoLabelLoader batch (get_labels rule on a device calc_dcd table, "
+                    "host distinct-source tables) + pinned-memory upload inside the timed loop"}
+
+
 def _free_port():
     so = socket.socket()
     so.bind(("127.0.0.1", 0))
@@ -434,6 +517,9 @@ def main():
                     help="skip the extra timed run that encodes every source slot")
     ap.add_argument("--no-k16-rate", action="store_true",
                     help="skip the extra timed run at 16 parts per target (no padding slots)")
+    ap.add_argument("--no-loader-rate", action="store_true",
+                    help="skip the extra timed run that takes every batch from the pseudo-label loader "
+                         "and uploads it inside the timed loop")
     ap.add_argument("--cpu-dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -541,6 +627,9 @@ def main():
         cfg["unique_sources"] = False      # every one of the B x 16 source slots encoded
         all_slots_rate = timed_rate(args.steps)
         cfg["unique_sources"] = True
+    loader = None
+    if not args.no_loader_rate and not args.no_extras:
+        loader = loader_rate(step, dict(cfg, unique_sources=True), db, dev, args.steps, world, rank)
     k16_rate = None
     if not args.no_k16_rate and args.parts != 16:
         # SURVEY §8(d)'s stress case: 16 parts per target, no padding slots (~200 distinct sources)
@@ -651,6 +740,9 @@ def main():
         extra["all_slots_iters_s"] = round(all_slots_rate, 4)
     if k16_rate is not None:
         extra["k16_iters_s"] = round(k16_rate, 4)
+    if loader is not None:
+        extra["loader_iters_s"] = loader["iters_s"]
+        extra["loader"] = loader
     extra["unique_sources"] = bool(cfg["unique_sources"])
     if not args.no_extras:
         ch = chamfer_rate(dev)

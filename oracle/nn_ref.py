@@ -95,3 +95,19 @@ def nn_seg_bwd(a, b, segs, gd_a, gd_b, idx_a, idx_b):
     ga = np.zeros_like(a); gb = np.zeros_like(b)
     _load().oracle_nn_seg_bwd(a, b, segs, segs.shape[0], _vp(gd_a), _vp(gd_b), _i32(idx_a), _i32(idx_b), ga, gb)
     return ga, gb
+
+
+def dist_chamfer(a, b):
+    """Restatement of the reference's Python chamfer, Density_aware_Chamfer_Distance/utils_v2/
+    metrics/CD/chamfer_python.py:18-39 (distChamfer): the dense float64 B x n x m matrix by the
+    expansion |x|^2 + |y|^2 - 2 x.y, min / argmin along both axes, cast to float32 / int32.
+    a [B,n,d], b [B,m,d] torch tensors. Used as the CPU baseline's chamfer (bench.py)."""
+    import torch
+    x, y = a.double(), b.double()
+    xx = (x * x).sum(2)
+    yy = (y * y).sum(2)
+    zz = torch.bmm(x, y.transpose(2, 1))
+    P = xx.unsqueeze(2) + yy.unsqueeze(1) - 2 * zz
+    m1, i1 = torch.min(P, 2)
+    m2, i2 = torch.min(P, 1)
+    return m1.float(), m2.float(), i1.int(), i2.int()

@@ -36,6 +36,18 @@ def test_nn_oracle_vs_distchamfer():
         np.testing.assert_array_equal(i2, g[case + "/i2"])
 
 
+def test_dist_chamfer_restatement_vs_reference():
+    """oracle.nn_ref.dist_chamfer (the CPU baseline's chamfer, bench.py) restates the reference's
+    chamfer_python.distChamfer: bit-exact on the reference-generated golden vectors."""
+    for case in ("u4x100x200", "u3x257x129", "u2x1x5", "u1x2048x2048", "grid"):
+        g = _g("nn_distchamfer.npz")
+        d1, d2, i1, i2 = nn_ref.dist_chamfer(torch.from_numpy(g[case + "/p1"]), torch.from_numpy(g[case + "/p2"]))
+        np.testing.assert_array_equal(d1.numpy(), g[case + "/d1"])
+        np.testing.assert_array_equal(d2.numpy(), g[case + "/d2"])
+        np.testing.assert_array_equal(i1.numpy(), g[case + "/i1"])
+        np.testing.assert_array_equal(i2.numpy(), g[case + "/i2"])
+
+
 def _direct_sq(q, r):
     q = q.astype(np.float32); r = r.astype(np.float32)
     dx = r[None, :, 0] - q[:, None, 0]; dy = r[None, :, 1] - q[:, None, 1]; dz = r[None, :, 2] - q[:, None, 2]
