@@ -63,6 +63,9 @@ class TargetEncoder(nn.Module):
         self.per_point_out = nn.Sequential(*_conv_bn_relu(1024, embedding_size)[:3],
                                            nn.Conv1d(embedding_size, embedding_size, 1))
         self.fc = nn.Linear(1024, embedding_size)
+        # parity diagnostics: when set, forward keeps the max-pool winners (last_pool_idx [G, 1024])
+        self.record_pool = False
+        self.last_pool_idx = None
 
     def _layers(self):
         convs = [(self.mlp1[0], self.mlp1[1]), (self.mlp1[3], self.mlp1[4]), (self.mlp2[0], self.mlp2[1]),
@@ -90,8 +93,12 @@ class TargetEncoder(nn.Module):
             sem = sem_f.reshape(B * n, -1)
             spec_mode = "tgt"
         bns, params = self._layers()
-        spec = EncoderSpec(spec_mode, n, self.training, bns, rw=rw)
+        rec = {} if self.record_pool else None
+        spec = EncoderSpec(spec_mode, n, self.training, bns, rw=rw, record=rec)
         code, pp = PointEncoderFn.apply(spec, xf.float(), sem.float(), *params)
+        if rec is not None:       # the max-pool winner of every (group, channel), within its group
+            G = rec["pool_rows"].shape[0]
+            self.last_pool_idx = rec["pool_rows"].long() - n * torch.arange(G, device=xf.device).unsqueeze(1)
         return code, pp
 
     def forward(self, x, sem_f):

@@ -32,13 +32,16 @@ class EncoderSpec:
     rw: optional K.RowWeights — group g of the call stands for rw.w[g] identical groups of
         the full batch (unique-row training: batch statistics and BN backward are those of
         the expanded batch; the caller expands outputs and sums duplicate gradients)
+    record: optional dict; the forward stores the max-pool winners there ("pool_rows": int32
+        [G, 1024], the row of the call each pooled channel came from)
     """
 
-    def __init__(self, mode, group_rows, training, bn_modules, momentum=0.1, eps=BN_EPS, rw=None):
+    def __init__(self, mode, group_rows, training, bn_modules, momentum=0.1, eps=BN_EPS, rw=None, record=None):
         assert mode in ("src", "tgt")
         self.mode, self.group_rows, self.training = mode, group_rows, training
         self.bn_modules, self.momentum, self.eps = bn_modules, momentum, eps
         self.rw = rw
+        self.record = record
 
 
 def _nbt(bnm):
@@ -119,6 +122,8 @@ class PointEncoderFn(Function):
         K.gemm(G, C, pooled.shape[1], pooled, pooled.shape[1], fcW, fcW.shape[1], code, C, bias=fcb)
         ctx.spec = spec
         ctx.states = states
+        if spec.record is not None:      # diagnostics / parity tests: the max-pool winners
+            spec.record["pool_rows"] = argidx
         ctx.save_for_backward(x, sem, pooled, argidx, *Ys, *params)
         return code, pp
 

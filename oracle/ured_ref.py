@@ -165,8 +165,39 @@ def bn(x, P, name, training=True):
                         P[name + ".weight"], P[name + ".bias"], training, BN_MOMENTUM, BN_EPS)
 
 
-def target_encoder(P, x, sem_f, is_src, training=True):
-    """network/simple_encoder.py:88-107. x: [B,N,3] (tgt) or [B,P,N,3] (src)."""
+POOL_TIE_TOL = 1e-4
+
+
+def max_pool(h, pool_idx=None, record=None, tie_tol=POOL_TIE_TOL):
+    """max_pool1d over points (simple_encoder.py:105): h [G, C, N] -> [G, C].
+
+    pool_idx (optional, [G, C] point index per channel): the winners another implementation
+    chose; they are taken instead of the argmax, after checking that each is a max up to
+    tie_tol of its channel's scale (an fp32 near-tie resolved the other way, not a wrong
+    point) — parity tests then compare gradients routed to the same points. record: gets
+    "argmax" (this function's own winners) and "overridden" (how many winners were taken)."""
+    mx, am = h.max(dim=2)
+    if record is not None:
+        record["argmax"] = am.detach()
+    if pool_idx is None:
+        return mx
+    idx = pool_idx.to(am.device).long()
+    chosen = h.gather(2, idx.unsqueeze(-1)).squeeze(-1)
+    scale = h.detach().abs().amax(dim=2) + 1e-12
+    gap = (mx - chosen).detach()
+    bad = gap > tie_tol * scale
+    if bool(bad.any()):
+        g, c = [int(v) for v in bad.nonzero()[0]]
+        raise AssertionError(f"max-pool winner {int(idx[g, c])} of group {g} channel {c} is "
+                             f"{float(gap[g, c]):.3e} below the max ({float(mx[g, c]):.6e}): not a near-tie")
+    if record is not None:
+        record["overridden"] = int((idx != am).sum())
+    return chosen
+
+
+def target_encoder(P, x, sem_f, is_src, training=True, pool_idx=None, record=None):
+    """network/simple_encoder.py:88-107. x: [B,N,3] (tgt) or [B,P,N,3] (src). pool_idx /
+    record: see max_pool."""
     if is_src:
         B, Pn, N, _ = x.shape
         x = x.reshape(B * Pn, N, 3)
@@ -185,7 +216,7 @@ def target_encoder(P, x, sem_f, is_src, training=True):
     h = F.relu(bn(conv(h, P, "fuse_sem.0"), P, "fuse_sem.1", training))
     pp = F.relu(bn(conv(h, P, "per_point_out.0"), P, "per_point_out.1", training))
     pp = conv(pp, P, "per_point_out.3")
-    g = h.max(dim=2).values
+    g = max_pool(h, pool_idx, record)
     g = F.linear(g, P["fc.weight"], P["fc.bias"])
     return g, pp
 
@@ -289,15 +320,38 @@ def get_symmetric(pc):
     return torch.cat([-pc[:, :, :1], pc[:, :, 1:2], pc[:, :, 2:3]], dim=2)
 
 
+NN_TIE_TOL = 1e-4
+
+
 class _OracleNN(torch.autograd.Function):
-    """Chamfer primitive on the C oracle (values and idx bit-exact to the contract)."""
+    """Chamfer primitive on the C oracle (values and idx bit-exact to the contract).
+
+    q1 (optional): another copy of p1 (e.g. the HIP step's fp32 deformed shape) from which the
+    NN indices of both directions are taken instead of p1's own. The distances are then those
+    of p1 / p2 at these indices, each checked to be the minimum up to NN_TIE_TOL (a near-tie
+    resolved the other way by the inputs' fp32-level differences, not a wrong neighbour), so a
+    parity test compares gradients routed to the same points."""
 
     @staticmethod
-    def forward(ctx, p1, p2):
-        d1, d2, i1, i2 = nn_ref.nn_fwd(p1.detach().float().numpy(), p2.detach().float().numpy())
+    def forward(ctx, p1, p2, q1=None):
+        a, b = p1.detach().float().numpy(), p2.detach().float().numpy()
+        d1, d2, i1, i2 = nn_ref.nn_fwd(a, b)
+        if q1 is not None:
+            _, _, i1, i2 = nn_ref.nn_fwd(np.ascontiguousarray(q1.detach().float().numpy()), b)
+            P1, P2 = p1.detach(), p2.detach()
+            bi = torch.arange(P1.shape[0]).unsqueeze(1)
+            e1 = ((P1 - P2[bi, torch.from_numpy(i1).long()]) ** 2).sum(-1)
+            e2 = ((P2 - P1[bi, torch.from_numpy(i2).long()]) ** 2).sum(-1)
+            for e, d, name in ((e1, d1, "p1 -> p2"), (e2, d2, "p2 -> p1")):
+                dd = torch.from_numpy(d).to(e.dtype)
+                bad = e > dd * (1 + NN_TIE_TOL) + 1e-10
+                if bool(bad.any()):
+                    raise AssertionError(f"given NN index ({name}) is {float((e - dd)[bad].max()):.3e} farther than "
+                                         "the nearest point: not a near-tie")
+            d1, d2 = e1.numpy(), e2.numpy()
         ctx.save_for_backward(p1, p2)
         ctx.idx = (i1, i2)
-        return torch.from_numpy(d1).to(p1.dtype), torch.from_numpy(d2).to(p1.dtype)
+        return torch.from_numpy(np.asarray(d1)).to(p1.dtype), torch.from_numpy(np.asarray(d2)).to(p1.dtype)
 
     @staticmethod
     def backward(ctx, g1, g2):
@@ -305,38 +359,54 @@ class _OracleNN(torch.autograd.Function):
         i1, i2 = ctx.idx
         r1, r2 = nn_ref.nn_bwd(p1.detach().float().numpy(), p2.detach().float().numpy(),
                                g1.float().numpy(), g2.float().numpy(), i1, i2)
-        return torch.from_numpy(r1).to(p1.dtype), torch.from_numpy(r2).to(p2.dtype)
+        return torch.from_numpy(r1).to(p1.dtype), torch.from_numpy(r2).to(p2.dtype), None
 
 
-def chamfer_costs(p1, p2):
-    """Shape_Measure ChamferLoss stand-in: squared NN distances (cost1 [B,n], cost2 [B,m])."""
-    return _OracleNN.apply(p1, p2)
+def chamfer_costs(p1, p2, q1=None):
+    """Shape_Measure ChamferLoss stand-in: squared NN distances (cost1 [B,n], cost2 [B,m]).
+    q1: optional index source for p1 (see _OracleNN)."""
+    return _OracleNN.apply(p1, p2, q1)
 
 
-def chamfer_distance2(p1, p2):
-    c1, c2 = chamfer_costs(p1, p2)
+def chamfer_distance2(p1, p2, q1=None):
+    c1, c2 = chamfer_costs(p1, p2, q1)
     return c1.mean(dim=1) + c2.mean(dim=1)
 
 
-def compute_cm_loss(source_p, target_p, target_part, mask=None, np_per_part=1024):
+def compute_cm_loss(source_p, target_p, target_part, mask=None, np_per_part=1024, source_q=None):
+    """source_q: optional NN index source for source_p (the same shape; see _OracleNN)."""
     if mask is None:
-        return chamfer_distance2(source_p, target_p)
+        return chamfer_distance2(source_p, target_p, source_q)
     n_valid = mask.sum(1) * np_per_part
+    q = (lambda sl: None) if source_q is None else (lambda sl: source_q[sl])
     full, part = [], []
     for b in range(source_p.shape[0]):
-        full.append(chamfer_distance2(source_p[b:b + 1, :int(n_valid[b].item())], target_p[b:b + 1]))
-        lp = [chamfer_distance2(source_p[b:b + 1, i * np_per_part:(i + 1) * np_per_part], tp.unsqueeze(0))
-              for i, tp in enumerate(target_part[b])]
+        sl = (slice(b, b + 1), slice(0, int(n_valid[b].item())))
+        full.append(chamfer_distance2(source_p[sl], target_p[b:b + 1], q(sl)))
+        lp = []
+        for i, tp in enumerate(target_part[b]):
+            sl = (slice(b, b + 1), slice(i * np_per_part, (i + 1) * np_per_part))
+            lp.append(chamfer_distance2(source_p[sl], tp.unsqueeze(0), q(sl)))
         part.append(torch.stack(lp).mean())
     return torch.stack(full).mean(), torch.stack(part).mean()
 
 
-def residual_retrieval_loss(x, x_source, residuals, mask, np_per_part=1024):
+def residual_retrieval_loss(x, x_source, residuals, mask, np_per_part=1024, source_q=None):
+    """source_q: optional NN index source for x_source (see _OracleNN)."""
     n_valid = mask.sum(1) * np_per_part
     nns = []
     for b in range(x.shape[0]):
         src = x_source[b, :int(n_valid[b].item())].detach()
-        _, idx = nn_ref.nn_dir(x[b].detach().float().numpy(), src.float().numpy())
+        xs = x[b].detach().float().numpy()
+        _, idx = nn_ref.nn_dir(xs, src.float().numpy())
+        if source_q is not None:
+            qs = np.ascontiguousarray(source_q[b, :int(n_valid[b].item())].detach().float().numpy())
+            d_own, _ = nn_ref.nn_dir(xs, src.float().numpy())
+            _, idx = nn_ref.nn_dir(xs, qs)
+            e = ((x[b].detach() - src[torch.from_numpy(idx).long()]) ** 2).sum(-1)
+            dd = torch.from_numpy(d_own).to(e.dtype)
+            if bool((e > dd * (1 + NN_TIE_TOL) + 1e-10).any()):
+                raise AssertionError("given kNN index is not a near-tie of the nearest point")
         nns.append(src[torch.from_numpy(idx).long()])
     nn = torch.stack(nns)
     res = x + residuals - nn
@@ -398,12 +468,16 @@ def train_forward(params, batch, cfg, training=True, epoch=0):
         x[:, :, 2] = -x[:, :, 2]
     B = x.shape[0]
 
-    codes, src_pp = target_encoder(params["src_encoder_all"], src_pts, src_sem_f, True, training)
+    pool = batch.get("_pool_idx", {})      # optional max-pool winners to follow (see max_pool)
+    prec = {"src_encoder_all": {}, "target_encoder_full": {}}
+    codes, src_pp = target_encoder(params["src_encoder_all"], src_pts, src_sem_f, True, training,
+                                   pool.get("src_encoder_all"), prec["src_encoder_all"])
     rin = torch.cat([codes.unsqueeze(2).expand(-1, -1, src_pp.shape[-1]), src_pp], dim=1)
     recon_src = residual_net(params["recon_decoder_src"], rin.permute(0, 2, 1), training)
     recon_src = recon_src.reshape(B, P_max, -1, 3)
 
-    tcode, pp = target_encoder(params["target_encoder_full"], x, tgt_sem_f, False, training)
+    tcode, pp = target_encoder(params["target_encoder_full"], x, tgt_sem_f, False, training,
+                               pool.get("target_encoder_full"), prec["target_encoder_full"])
     pp = pp.permute(0, 2, 1)
     part_f, re_in, mask, part_x, param_def = get_part(pp, batch["labels"], x, P_max)
     N = pp.shape[1]
@@ -415,14 +489,18 @@ def train_forward(params, batch, cfg, training=True, epoch=0):
     out = get_shape(mats, prm, param_def, cfg["alpha"]).reshape(B, -1, 3)
 
     T = OrderedDict()
+    # optional NN index source: the HIP step's fp32 deformed shape (see _OracleNN)
+    oq = batch.get("_nn_out")
     use_param = cfg.get("use_param_loss", 0.0) > 0.0
     if use_param:
         T["param_loss"] = regularization_param(prm, mask)
-    T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask)
+    T["cd_loss_full"], T["cd_loss_part"] = compute_cm_loss(out, x, part_x, mask, source_q=oq)
     T["contrast_loss"] = contrast_loss(part_f, codes, batch["src_labels"])
-    T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(get_symmetric(out), x, part_x, mask)
+    T["ref_cd_loss_full"], T["ref_cd_loss_part"] = compute_cm_loss(
+        get_symmetric(out), x, part_x, mask, source_q=None if oq is None else get_symmetric(oq))
     if epoch > cfg["init_p_m_loss"]:
-        T["re_reg_loss_full"], T["reg_loss_full"] = residual_retrieval_loss(x, out.detach(), re_res, mask)
+        T["re_reg_loss_full"], T["reg_loss_full"] = residual_retrieval_loss(x, out.detach(), re_res, mask,
+                                                                            source_q=oq)
     T["recon_loss_full"] = pc_consistency(recon_full, x)
     T["recon_loss_src"] = pc_consistency_weighted(recon_src, src_pts, mask)
     loss = T["param_loss"] * cfg["use_param_loss"] if use_param else 0.0
@@ -434,6 +512,7 @@ def train_forward(params, batch, cfg, training=True, epoch=0):
     T["all_loss"] = loss
     T["_out"] = out
     T["_params"] = prm
+    T["_pool"] = prec
     return loss, T
 
 

@@ -17,8 +17,9 @@ Tolerances (tests/step_parity.py, same rules as tests/test_train_step_gpu.py):
   * every loss term within 1e-5 relative (SURVEY §8(d)); the deviations are printed;
   * the deformed shape within 1e-4 of its largest coordinate;
   * every parameter gradient tensor compared whole: ||g - g_ref|| / ||g_ref|| <= 1e-3 and the
-    elementwise max deviation within 2e-3 of the tensor's largest entry; the exactly-zero true
-    gradients (BN-fed conv biases, attention key biases) at noise level;
+    elementwise max deviation within 2e-3 of the tensor's largest entry, or 3x the deviation of
+    the same oracle run in fp32 where fp32 accumulation alone moves a tensor further; the
+    exactly-zero true gradients (BN-fed conv biases, attention key biases) at noise level;
   * NN distances and indices of the step's own chamfer families bit-exact against the C oracle
     run on the same (GPU-produced) inputs and segment tables;
   * retrieval indices bit-exact except where the oracle's top-2 cosine gap is < 1e-6 (SURVEY
@@ -81,20 +82,44 @@ def _oracle_batch(db_np, bt, dtype=torch.float64):
     return ob
 
 
-def _oracle_step(key, cfg, db_np, bt):
-    """float64 oracle forward + backward, cached per configuration: (terms, out, gradients)."""
+def _grads_of(P):
+    return {(mod, k): (None if v.grad is None else v.grad.detach().clone())
+            for mod, sd in P.items() if mod != "embedding_layer"
+            for k, v in sd.items() if torch.is_tensor(v) and v.requires_grad}
+
+
+def _oracle_floor(key, cfg, db_np, bt):
+    """The oracle's gradients from an fp32 run (its own max-pool / NN choices), cached per
+    configuration: the per-tensor fp32 noise floor of tests/step_parity.py."""
     if key not in _ORACLE:
         _threads()
-        _, P64 = _params64(cfg, seed=7)
-        loss, R = ured_ref.train_forward(P64, _oracle_batch(db_np, bt), cfg)
+        P, _ = _params64(cfg, seed=7)
+        P32 = {m: {k: (v.clone().requires_grad_(True) if v.dtype.is_floating_point and "running" not in k else v.clone())
+                   for k, v in sd.items()} for m, sd in P.items()}
+        loss, R = ured_ref.train_forward(P32, _oracle_batch(db_np, bt, torch.float32), cfg)
         loss.backward()
-        terms = {k: float(R[k]) for k in TERMS}
-        grads = {(mod, k): (None if v.grad is None else v.grad.detach().clone())
-                 for mod, sd in P64.items() if mod != "embedding_layer"
-                 for k, v in sd.items() if torch.is_tensor(v) and v.requires_grad}
-        _ORACLE[key] = (terms, R["_out"].detach().float(), grads)
-        del loss, R, P64
+        _ORACLE[key] = _grads_of(P32)
+        del loss, R, P32
     return _ORACLE[key]
+
+
+def _oracle64(cfg, db_np, bt, pool_idx=None, nn_out=None):
+    """float64 oracle forward + backward -> (terms, out, gradients, its max-pool record).
+    pool_idx / nn_out: the HIP step's max-pool winners and deformed shape, whose discrete choices
+    (max-pool winners, NN indices) the oracle follows where they are near-ties of its own
+    (ured_ref.max_pool, ured_ref._OracleNN: each checked, a non-tie raises)."""
+    _threads()
+    _, P64 = _params64(cfg, seed=7)
+    ob = _oracle_batch(db_np, bt)
+    if pool_idx is not None:
+        ob["_pool_idx"] = pool_idx
+    if nn_out is not None:
+        ob["_nn_out"] = nn_out
+    loss, R = ured_ref.train_forward(P64, ob, cfg)
+    loss.backward()
+    res = ({k: float(R[k]) for k in TERMS}, R["_out"].detach().float(), _grads_of(P64), R["_pool"])
+    del loss, R, P64
+    return res
 
 
 def _run_step(dev, B, N, parts, unique, data_seed=4):
@@ -119,16 +144,21 @@ def _check_step(dev, B, N, parts, unique):
     if unique:
         U = batch["src_unique"].U
         assert U < B * 16
+    step_parity.record_pools(ts.models)
     loss, T = ts.forward(batch)
-    got_terms = {k: float(T[k]) for k in TERMS}
+    got_terms = {k: float(T[k].detach()) for k in TERMS}
     out = T["_out"].detach()
     loss.backward()
-    rterms, rout, rgrads = _oracle_step((B, N, parts), cfg, db_np, bt)
     label = f"B={B} N={N} k={parts} unique={unique}"
+    rgrads32 = _oracle_floor((B, N, parts), cfg, db_np, bt)
+    choices = step_parity.gpu_pool_choices(ts.models, batch, unique)
+    rterms, rout, rgrads, rpool = _oracle64(cfg, db_np, bt, choices, out.cpu())
+    print(f"\n{label}: max-pool winners taken from the HIP step where they differ (ties): " +
+          ", ".join(f"{n} {rpool[n]['overridden']}" for n in step_parity.ENCODERS))
     step_parity.check_loss_terms(got_terms, rterms, label)
     o = out.cpu()
     assert (o - rout).abs().max().item() <= 1e-4 * rout.abs().max().item()
-    n, _ = step_parity.check_grads(ts.models, rgrads, label)
+    n, _ = step_parity.check_grads(ts.models, rgrads, label, ref32=rgrads32)
     assert n >= 145
     _check_step_nn(out, batch, cfg)
     return got_terms

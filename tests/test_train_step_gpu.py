@@ -66,6 +66,18 @@ def _oracle_grads(P):
             for k, v in sd.items() if torch.is_tensor(v) and v.requires_grad}
 
 
+def _oracle_grads32(P, ob, cfg):
+    """The same oracle step in fp32: the per-tensor fp32 noise floor (tests/step_parity.py)."""
+    P32 = {m: {k: (v.detach().float().requires_grad_(True) if v.dtype.is_floating_point and "running" not in k
+                   else v.detach().float() if v.dtype.is_floating_point else v.detach().clone())
+               for k, v in sd.items()} for m, sd in P.items()}
+    ob32 = {k: (v.float() if v.dtype.is_floating_point else v) for k, v in ob.items()
+            if not k.startswith("_")}          # its own discrete choices: the fp32 noise floor
+    loss, _ = ured_ref.train_forward(P32, ob32, cfg)
+    loss.backward()
+    return _oracle_grads(P32)
+
+
 @pytest.mark.parametrize("unique", [True, False], ids=["unique_sources", "all_slots"])
 @pytest.mark.parametrize("N,parts", [(128, (3, 2)), (512, (4, 4)), (256, (16, 1))])
 def test_train_step_matches_oracle(dev, N, parts, unique):
@@ -75,7 +87,12 @@ def test_train_step_matches_oracle(dev, N, parts, unique):
     ts, batch, P, ob, cfg = _setup(dev, N=N, parts=parts, unique=unique)
     if unique:
         assert batch["src_unique"].U < 2 * 16   # padding slots collapse onto one source part
+    step_parity.record_pools(ts.models)
     loss, T = ts.forward(batch)
+    # the oracle routes each pooled gradient to the point the HIP step chose (checked to be a
+    # max up to fp32 noise: near-ties may resolve either way under a different summation order)
+    ob["_pool_idx"] = step_parity.gpu_pool_choices(ts.models, batch, unique)
+    ob["_nn_out"] = T["_out"].detach().cpu()      # NN indices: the HIP step's near-tie choices too
     rloss, R = ured_ref.train_forward(P, ob, cfg)
     label = f"N={N} parts={parts} unique={unique}"
     step_parity.check_loss_terms({k: T[k].item() for k in TERMS}, {k: R[k].item() for k in TERMS}, label)
@@ -83,7 +100,7 @@ def test_train_step_matches_oracle(dev, N, parts, unique):
     assert (o - ro).abs().max().item() <= 1e-4 * ro.abs().max().item()
     loss.backward()
     rloss.backward()
-    n, _ = step_parity.check_grads(ts.models, _oracle_grads(P), label)
+    n, _ = step_parity.check_grads(ts.models, _oracle_grads(P), label, ref32=_oracle_grads32(P, ob, cfg))
     assert n >= 145
 
 
@@ -96,14 +113,17 @@ def test_train_step_param_loss_complementme(dev, case):
     over = {"param_loss": {"use_param_loss": 1.0}, "complementme": {"complementme": True},
             "both": {"use_param_loss": 0.5, "complementme": True}}[case]
     ts, batch, P, ob, cfg = _setup(dev, N=256, parts=(4, 2), **over)
+    step_parity.record_pools(ts.models)
     loss, T = ts.forward(batch)
+    ob["_pool_idx"] = step_parity.gpu_pool_choices(ts.models, batch, True)
+    ob["_nn_out"] = T["_out"].detach().cpu()
     rloss, R = ured_ref.train_forward(P, ob, cfg)
     terms = TERMS + (("param_loss",) if "use_param_loss" in over else ())
     assert ("param_loss" in T) == ("use_param_loss" in over)
     step_parity.check_loss_terms({k: T[k].item() for k in terms}, {k: R[k].item() for k in terms}, case)
     loss.backward()
     rloss.backward()
-    step_parity.check_grads(ts.models, _oracle_grads(P), case)
+    step_parity.check_grads(ts.models, _oracle_grads(P), case, ref32=_oracle_grads32(P, ob, cfg))
     if "complementme" in over:      # the flip really happened: the un-flipped step differs
         ts2, batch2, _, _, _ = _setup(dev, N=256, parts=(4, 2))
         _, T2 = ts2.forward(batch2)
