@@ -567,10 +567,11 @@ int fused_dispatch(NNFusedArgs a, int nseg, int max_a, int max_b, void* ws, size
     return 0;
 }
 
-int bwd_dispatch(const NNBwdArgs& a, int nseg, int max_a, int max_b, hipStream_t st) {
-    const int max_p = max(max_a, max_b);
+// sides = 2: a and b points; 1: the a points only (blockIdx.z = 0)
+int bwd_dispatch(const NNBwdArgs& a, int nseg, int max_a, int max_b, hipStream_t st, int sides = 2) {
+    const int max_p = sides == 2 ? max(max_a, max_b) : max_a;
     if (max_p <= 0 || nseg <= 0) return 0;
-    dim3 grid((max_p + NN_THREADS - 1) / NN_THREADS, nseg, 2);
+    dim3 grid((max_p + NN_THREADS - 1) / NN_THREADS, nseg, sides);
     hipLaunchKernelGGL(nn_bwd_kernel, grid, dim3(NN_THREADS), 0, st, a);
     return 0;
 }
@@ -859,9 +860,9 @@ int ured_nn_seg_bwd(const float* a, const float* b, const int* segs, int nseg,
     URED_REQUIRE(nseg >= 0 && max_a_len >= 0 && max_b_len >= 0, "ured_nn_seg_bwd: negative size");
     URED_REQUIRE(nseg <= 65535, "ured_nn_seg_bwd: nseg %d exceeds 65535", nseg);
     if (nseg == 0) return 0;
-    URED_REQUIRE(a && b && segs && idx_a && idx_b && ga && gb, "ured_nn_seg_bwd: null pointer");
+    URED_REQUIRE(a && b && segs && idx_a && idx_b && ga, "ured_nn_seg_bwd: null pointer");
     NNBwdArgs A{a, b, reinterpret_cast<const int4*>(segs), 0, 0, gd_a, gd_b, idx_a, idx_b, ga, gb};
-    bwd_dispatch(A, nseg, max_a_len, max_b_len, (hipStream_t)stream);
+    bwd_dispatch(A, nseg, max_a_len, max_b_len, (hipStream_t)stream, gb ? 2 : 1);
     return ured::launch_status("ured_nn_seg_bwd");
 }
 

@@ -128,10 +128,13 @@ class TrainStep:
                             if dev.type == "cuda" and cfg.get("stream_overlap", False) else None)
         self.deform_stream = (torch.cuda.Stream(device=dev)
                               if dev.type == "cuda" and cfg.get("deform_overlap", False) else None)
+        # the fused HIP loss head (ured_hip/losshead.py); False: the composed torch + NN-launch form
+        self.loss_head = dev.type == "cuda" and cfg.get("loss_head", True) and not cfg.get("stream_overlap", False)
 
-    def _source_branch(self, uq, src_points, src_sem_f, B, P):
+    def _source_branch(self, uq, src_points, src_sem_f, B, P, expand_rec=True):
         """src_encoder_all + recon_decoder_src (engine/train.py:210-216) -> codes [B*P, C],
-        recon_src_p [B, P, NP, 3]."""
+        recon_src_p [B, P, NP, 3] — or, with expand_rec=False, (codes, recon per encoded part
+        [U, NP, 3], that part's points [U, NP, 3], slot -> part index [B*P]) for the loss head."""
         M = self.models
         if uq is not None:
             # unique source encoding: the slots' inputs are functions of their source part
@@ -140,15 +143,26 @@ class TrainStep:
             rw = RowWeights(uq.w, self.np_per_part)
             with torch.no_grad():
                 sem_u = M["embedding_layer"](self.db.sem[uq.uniq])
-            code_u, pp_u = M["src_encoder_all"].forward_pointmajor(self.db.points[uq.uniq].unsqueeze(0),
-                                                                   sem_u.unsqueeze(0), rw=rw)
+            pts_u = self.db.points[uq.uniq]
+            code_u, pp_u = M["src_encoder_all"].forward_pointmajor(pts_u.unsqueeze(0), sem_u.unsqueeze(0), rw=rw)
             rec_u = M["recon_decoder_src"].forward_split(pp_u, code_u, code_first=True,
                                                          group_rows=self.np_per_part, rw=rw)
+            if not expand_rec:
+                return uq.expand(code_u), rec_u.view(uq.U, -1, 3), pts_u, uq.inverse
             return uq.expand(code_u), uq.expand(rec_u.view(uq.U, -1)).view(B, P, -1, 3)
         codes, src_pp = M["src_encoder_all"].forward_pointmajor(src_points, src_sem_f)
         recon_src_p = M["recon_decoder_src"].forward_split(src_pp, codes, code_first=True,
                                                            group_rows=self.np_per_part).view(B, P, -1, 3)
+        if not expand_rec:
+            return (codes, recon_src_p.view(B * P, -1, 3), src_points.reshape(B * P, -1, 3),
+                    self._arange(B * P, codes.device))
         return codes, recon_src_p
+
+    def _arange(self, n, dev):
+        a = getattr(self, "_ar", None)
+        if a is None or a.shape[0] != n:
+            a = self._ar = torch.arange(n, device=dev)
+        return a
 
     def _deform_losses(self, T, tcode, codes, mats, param_def, x, part_x, mask_part, target_part_f, src_labels):
         """param_decoder_full -> get_shape -> chamfer (full, part), contrast and symmetry terms
@@ -186,6 +200,74 @@ class TrainStep:
         return loss, out, params_full, knn_idx
 
     def forward(self, batch, epoch=0):
+        if self.loss_head:
+            return self._forward_head(batch, epoch)
+        return self._forward_composed(batch, epoch)
+
+    def _forward_head(self, batch, epoch=0):
+        """The step with the loss head as one HIP autograd Function (ured_hip/losshead.py): the
+        chamfer, contrastive, residual and reconstruction losses and their weighted sum in ~10
+        launches forward and ~7 backward (the composed form, _forward_composed, is the same
+        arithmetic as ~150 small torch kernels)."""
+        from loss.contrast_loss import get_world_size
+        from ured_hip.losshead import HeadInputs, loss_head
+        cfg, M = self.cfg, self.models
+        P = cfg["MAX_NUM_PARTS"]
+        x = batch["x"]
+        if cfg.get("complementme", False):      # engine/train.py:192-194 (out of place, see _forward_composed)
+            x = x * self._zflip
+        B, N, _ = x.shape
+        src_labels = batch["src_labels"]
+        uq = batch.get("src_unique") if cfg.get("unique_sources", True) else None
+        mats, _, src_sem_idx = get_source_info(src_labels, self.db)
+        emb = M["embedding_layer"]
+        with torch.no_grad():          # the embedding is not trained (optimizer_dm.py:83)
+            src_sem_f = emb(src_sem_idx) if uq is None else None
+            tgt_sem_f = emb(batch["tgt_sem"])
+        # every slot's points only when every slot is encoded (the unique path reads the distinct parts)
+        src_points = get_source_points(src_labels, self.db) if uq is None else None
+        codes, rec_u, pts_u, inv = self._source_branch(uq, src_points, src_sem_f, B, P, expand_rec=False)
+        tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
+        target_part_f, _, re_in, mask_part, parts, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
+        codes = codes.view(B, P, -1)
+        dside = self.deform_stream
+        if dside is not None:
+            # DeformNet + get_shape (latency-bound small kernels) on their own stream, overlapping
+            # the GEMM-bound residual / reconstruction nets (autograd runs each node's backward on
+            # its forward stream)
+            main = torch.cuda.current_stream(x.device)
+            dside.wait_stream(main)
+            for t in (tcode, codes, mats, param_def):
+                t.record_stream(dside)
+            with torch.cuda.stream(dside):
+                params_full = M["param_decoder_full"](tcode, codes, None)
+                out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
+        else:
+            params_full = M["param_decoder_full"](tcode, codes, None)
+            out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
+        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
+        re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
+                                                         off=re_in.off).view(B, N, 3)
+        if dside is not None:
+            main.wait_stream(dside)
+            out.record_stream(main)
+            params_full.record_stream(main)
+        param = regularization_param(params_full, mask_part) if cfg.get("use_param_loss", 0.0) > 0.0 else None
+        contrast_ext = None
+        if get_world_size() > 1 and cfg.get("use_contrast_loss", 0.0) > 0.0:
+            # the reference gathers the source codes of every rank (contrast_loss.py:35-58)
+            contrast_labels = torch.where(src_labels >= 0, torch.ones_like(src_labels), src_labels)
+            contrast_ext = compute_contrast_loss_loss(target_part_f, codes, contrast_labels,
+                                                      cfg.get("differentiable_gather", False))
+        hi = HeadInputs(x, parts, self.np_per_part, src_labels, pts_u, inv, cfg,
+                        gate=cfg.get("use_residuals_reg", 0.0) > 0.0 and epoch > cfg["init_p_m_loss"])
+        loss, T, _ = loss_head(hi, out, re_res, recon_full_p, rec_u, target_part_f, codes, param, contrast_ext)
+        T["all_loss"] = loss
+        T["_out"] = out
+        T["_params"] = params_full
+        return loss, T
+
+    def _forward_composed(self, batch, epoch=0):
         cfg, M = self.cfg, self.models
         P = cfg["MAX_NUM_PARTS"]
         x = batch["x"]

@@ -8,5 +8,6 @@
   optim    FlatAdam: per-module gradient clipping + Adam over flat buffers
   node     DeformNet graph-node GEMM / BatchNorm launches
   ops      device-side part building (segment sums, AABBs)
+  losshead the step's loss head (chamfer families, contrastive, residual, reconstruction, weighted sum)
 """
-from . import _lib, attn, kernels, nn, node, ops, optim  # noqa: F401
+from . import _lib, attn, kernels, losshead, nn, node, ops, optim  # noqa: F401

@@ -126,7 +126,8 @@ int ured_emd_bwd(const float* xyz1, const float* xyz2, int b, int n, const float
                  float* gradxyz1, void* stream);
 
 /* Backward of ured_nn_seg_fwd: accumulates into ga (a-points) and gb (b-points)
- * exactly the per-pair formula of ured_nn_bwd. gd_a / gd_b may be NULL. */
+ * exactly the per-pair formula of ured_nn_bwd. gd_a / gd_b may be NULL; gb may be NULL when
+ * the b points need no gradient (only the a side is computed). */
 int ured_nn_seg_bwd(const float* a, const float* b, const int* segs, int nseg,
                     int max_a_len, int max_b_len,
                     const float* gd_a, const float* gd_b, const int* idx_a, const int* idx_b,
@@ -384,6 +385,69 @@ typedef struct {
     float* dgamma; float* dbeta; int accumulate;
 } UredNodeBNBwdDesc;
 int ured_node_bn_bwd(const UredNodeBNBwdDesc* d, void* stream);
+
+
+/* ---------------- loss head (csrc/loss.hip) ---------------- */
+/* compute_cm_loss of the deformed shape `out` [B,S,3] and of its mirror image (x -> -x,
+ * get_symmetric) against the same target x [B,N,3] (engine/train.py:288,302 ->
+ * loss/chamfer_loss.py:13-30, the Shape_Measure ChamferLoss calls per sample and per part):
+ *   prep   : A = [out; mirror(out)] [2B,S,3], X2 = [x; x], XS2 = [x_sorted; x_sorted] [2B,N,3] and
+ *            the segment tables of ured_nn_seg_fwd: full family int32 [2B,4] (a = the first
+ *            k_b*NP points of half-sample s, b = its x) and part family [2B*P,4] (chunk i < k_b of
+ *            NP points vs the points of part i: off int32 [B*P+1] / counts int64 [B,P] of
+ *            x_sorted, k int64 [B] parts per sample);
+ *   reduce : the four scalars [full, part, mirror full, mirror part] from the two families' NN
+ *            distances (dist_a_* [2B*S], dist_b_* [2B*N]); CD = mean(cost1) + mean(cost2), part
+ *            CD = mean over the sample's parts, both averaged over B. ws: 3*2B*(P+1) floats;
+ *            counter: a device uint that is 0 before the launch (it is left at 0);
+ *   grad   : d terms g4 [4] -> the per-distance upstream weights of ured_nn_seg_bwd (gid int32
+ *            [B*N]: part slot of each sorted row) and ga [2B*S*3] zeroed for its accumulation;
+ *   fold   : grad_out [B,S,3] = ga[:B] + mirror(ga[B:]).
+ * Replace the per-sample / per-part Python loops, means and masks of the reference (and their
+ * autograd) with 4 + 3 launches around the two NN launches. */
+int ured_cd_pair_prep(const float* out, const float* x, const float* x_sorted, const long long* k,
+                      const long long* counts, const int* off, int B, int S, int N, int P, int NP, float* A,
+                      float* X2, float* XS2, int* segs_full, int* segs_part, void* stream);
+int ured_cd_pair_reduce(const float* dist_a_full, const float* dist_b_full, const float* dist_a_part,
+                        const float* dist_b_part, const long long* k, const long long* counts, const int* off,
+                        int B, int S, int N, int P, int NP, float* ws, unsigned* counter, float* terms, void* stream);
+int ured_cd_pair_grad(const float* g4, const long long* k, const long long* counts, const int* gid, int B, int S,
+                      int N, int P, int NP, float* gd_a_full, float* gd_b_full, float* gd_a_part, float* gd_b_part,
+                      float* ga, void* stream);
+int ured_cd_pair_fold(const float* ga, int B, int S, float* grad_out, void* stream);
+
+/* residual_retrieval_loss (loss/basic_loss.py:249-265: x -> out nearest neighbour knn [B,N]
+ * relative to the sample's rows, terms mean_n sum|x + res - out[nn]| and mean_n sum|res|),
+ * compute_pc_consistency(rec, x) and compute_pc_consistency_weighted(recon_src, src_points, mask)
+ * (loss/basic_consistency_loss.py:4-22), the last over the U distinct source parts of the batch
+ * (recu / ptsu [U,NP,3]; slot r of the R = B*P part slots holds part inv[r], weight mask[r]).
+ * Forward -> terms [4]; backward: upstream g4 [4] -> dres, drec [B,N,3], drecu [U,NP,3]. */
+typedef struct {
+    int B, N, S, U, NP, R;
+    const float* x; const float* out; const int* knn; const float* res; const float* rec;
+    const float* recu; const float* ptsu; const long long* inv; const float* mask;
+} UredPointLossDesc;
+int ured_point_losses_fwd(const UredPointLossDesc* d, float* ws, unsigned* counter, float* terms, void* stream);
+int ured_point_losses_bwd(const UredPointLossDesc* d, const float* g4, float* dres, float* drec, float* drecu,
+                          void* stream);
+
+/* compute_contrast_loss_loss (loss/contrast_loss.py:61-102): t [n,C] target part features,
+ * s_all [n_all,C] source codes of every rank (this rank's rows start at s_off), src_labels int64
+ * [n] (-1: row ignored, else its label is s_off + i); loss = CE(scale * norm(t) norm(s_all)^T).
+ * Forward writes inv norms [n + n_all], lse [n], ws [2n] and loss [1]; backward (g: d loss)
+ * writes dt [n,C] and, when ds is not NULL, ds [n,C] for this rank's rows. */
+int ured_contrast_fwd(const float* t, const float* s_all, const long long* src_labels, int n, int n_all, int C,
+                      int s_off, float scale, float* inv, float* lse, float* ws, unsigned* counter, float* loss,
+                      void* stream);
+int ured_contrast_bwd(const float* t, const float* s_all, const long long* src_labels, int n, int n_all, int C,
+                      int s_off, float scale, const float* inv, const float* lse, const float* g, float* dt, float* ds,
+                      void* stream);
+
+/* loss_all = sum_i weights[i] * *terms[i] in order (engine/train.py:278-335), one thread; the
+ * backward writes gterms[i] = weights[i] * g. */
+#define URED_ASSEMBLE_MAX 16
+int ured_loss_assemble(int K, const float* const* terms, const float* weights, float* out, void* stream);
+int ured_loss_assemble_bwd(int K, const float* weights, const float* g, float* gterms, void* stream);
 
 #ifdef __cplusplus
 }
