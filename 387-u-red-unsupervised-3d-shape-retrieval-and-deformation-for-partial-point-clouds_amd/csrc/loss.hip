@@ -131,12 +131,15 @@ __global__ __launch_bounds__(LT) void cd_pair_prep_kernel(CdShape sh, const floa
 // full family's b-side sum over x. The last workgroup combines (fp64, fixed order):
 //   full_s = sum_a / (k_b NP) + sum_b / N,  part_s = (1/k_b) sum_{i<k_b} (a_i / NP + b_i / cnt_i)
 //   terms  = [mean_b full (h=0), mean_b part (h=0), mean_b full (h=1), mean_b part (h=1)].
+constexpr int CD_MAX_UNITS = 2 * 128 * 33;    // 2B (P+1) partial units staged in LDS (B <= 128, P <= 32)
+
 __global__ __launch_bounds__(LT) void cd_pair_reduce_kernel(CdShape sh, const float* __restrict__ daf,
         const float* __restrict__ dbf, const float* __restrict__ dap, const float* __restrict__ dbp,
         const long long* __restrict__ k, const long long* __restrict__ counts, const int* __restrict__ off,
         float* __restrict__ part, unsigned* counter, float* __restrict__ terms) {
     __shared__ float shf[LT];
     __shared__ double shd[LT];
+    extern __shared__ float stage[];           // last workgroup: 3 * 2B(P+1) partials
     const int i = blockIdx.x, s = blockIdx.y;
     const int h = s / sh.B, b = s % sh.B;
     const int kb = (int)k[b];
@@ -162,6 +165,9 @@ __global__ __launch_bounds__(LT) void cd_pair_reduce_kernel(CdShape sh, const fl
     const int slot = s * (sh.P + 1) + i;
     if (t == 0) { part[3 * slot] = q0; part[3 * slot + 1] = q1; part[3 * slot + 2] = q2; }
     if (!last_arrival(counter, gridDim.x * gridDim.y)) return;
+    const int units = 2 * sh.B * (sh.P + 1);
+    for (int q = t; q < 3 * units; q += LT) stage[q] = ld_agent(part + q);   // independent loads
+    __syncthreads();
     // combine: one thread per half-sample, then the batch means
     double fs = 0.0, ps = 0.0;
     int hh = 0;
@@ -172,11 +178,11 @@ __global__ __launch_bounds__(LT) void cd_pair_reduce_kernel(CdShape sh, const fl
         double sa = 0.0, sp = 0.0;
         for (int ii = 0; ii < kk; ++ii) {
             const int sl = ss * (sh.P + 1) + ii;
-            sa += (double)ld_agent(part + 3 * sl);
+            sa += (double)stage[3 * sl];
             const double cnt = (double)counts[(size_t)bb * sh.P + ii];
-            sp += (double)ld_agent(part + 3 * sl + 1) / sh.NP + (cnt > 0 ? (double)ld_agent(part + 3 * sl + 2) / cnt : 0.0);
+            sp += (double)stage[3 * sl + 1] / sh.NP + (cnt > 0 ? (double)stage[3 * sl + 2] / cnt : 0.0);
         }
-        const double sbf = (double)ld_agent(part + 3 * (ss * (sh.P + 1) + sh.P));
+        const double sbf = (double)stage[3 * (ss * (sh.P + 1) + sh.P)];
         fs = kk > 0 ? sa / ((double)kk * sh.NP) + sbf / sh.N : __builtin_nan("");
         ps = kk > 0 ? sp / kk : __builtin_nan("");
     }
@@ -255,7 +261,7 @@ struct PointLossArgs {
     float* dres; float* drec; float* drecu;  // backward outputs
 };
 
-constexpr int PL_CHUNK = 1024;               // points per workgroup of the B*N part
+constexpr int PL_CHUNK = 256;                // points per workgroup of the B*N part
 
 __device__ __forceinline__ float slot_weight(const PointLossArgs& a, int u, float* shf, float* msum) {
     // w_u = sum of the mask over the slots that hold distinct part u; *msum = sum of the mask
@@ -385,17 +391,29 @@ __global__ __launch_bounds__(LT) void contrast_norms_kernel(ContrastArgs a) {
     if (threadIdx.x == 0) a.inv[r] = 1.f / fmaxf(sqrtf(q), 1e-12f);
 }
 
+// dot(v (LDS), row (global)) by ONE thread: float4 loads (C % 4 == 0, 16-B aligned rows), four
+// independent accumulators so that several loads are in flight per lane
+__device__ __forceinline__ float row_dot(const float* v, const float* row, int C) {
+    const float4* r4 = reinterpret_cast<const float4*>(row);
+    const float4* v4 = reinterpret_cast<const float4*>(v);
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+    const int C4 = C >> 2;
+#pragma unroll 4
+    for (int q = 0; q < C4; ++q) {
+        const float4 a = r4[q], b = v4[q];
+        d0 += a.x * b.x; d1 += a.y * b.y; d2 += a.z * b.z; d3 += a.w * b.w;
+    }
+    return (d0 + d1) + (d2 + d3);
+}
+
 // logits of t row i against every s row into lg[] (LDS): scale * (t_i . s_j) * inv_t * inv_s
+// (thread j takes row j: 256 rows in flight per workgroup)
 __device__ __forceinline__ void logits_row(const ContrastArgs& a, int i, float* trow, float* lg) {
     for (int c = threadIdx.x; c < a.C; c += LT) trow[c] = a.t[(size_t)i * a.C + c];
     __syncthreads();
     const float it = a.inv[i] * a.scale;
-    for (int j = threadIdx.x; j < a.n_all; j += LT) {
-        const float* sj = a.s + (size_t)j * a.C;
-        float d = 0.f;
-        for (int c = 0; c < a.C; ++c) d += trow[c] * sj[c];
-        lg[j] = d * it * a.inv[a.n + j];
-    }
+    for (int j = threadIdx.x; j < a.n_all; j += LT)
+        lg[j] = row_dot(trow, a.s + (size_t)j * a.C, a.C) * it * a.inv[a.n + j];
     __syncthreads();
 }
 
@@ -477,10 +495,7 @@ __global__ __launch_bounds__(LT) void contrast_bwd_kernel(ContrastArgs a) {
     const float isj = a.inv[a.n + j];
     // column j of the logits and its gradient, for every t row i
     for (int i = t; i < a.n; i += LT) {
-        const float* ti = a.t + (size_t)i * a.C;
-        float d = 0.f;
-        for (int c = 0; c < a.C; ++c) d += ti[c] * row[c];
-        const float lg = d * a.inv[i] * a.scale * isj;
+        const float lg = row_dot(row, a.t + (size_t)i * a.C, a.C) * a.inv[i] * a.scale * isj;
         const bool valid = a.src_labels[i] != -1;
         dl[i] = valid ? gsc * (expf(lg - a.lse[i]) - (j == a.s_off + i ? 1.f : 0.f)) * a.scale * a.inv[i] : 0.f;
     }
@@ -540,10 +555,12 @@ int ured_cd_pair_reduce(const float* dist_a_full, const float* dist_b_full, cons
                         const float* dist_b_part, const long long* k, const long long* counts, const int* off,
                         int B, int S, int N, int P, int NP, float* ws, unsigned* counter, float* terms, void* stream) {
     ured::clear_error();
-    URED_REQUIRE(B > 0 && 2 * B <= LT && S > 0 && N > 0 && P > 0 && NP > 0, "ured_cd_pair_reduce: bad sizes");
+    URED_REQUIRE(B > 0 && 2 * B <= LT && S > 0 && N > 0 && P > 0 && NP > 0 && 2 * B * (P + 1) <= CD_MAX_UNITS,
+                 "ured_cd_pair_reduce: bad sizes");
     URED_REQUIRE(dist_a_full && dist_b_full && dist_a_part && dist_b_part && k && counts && off && ws && counter && terms,
                  "ured_cd_pair_reduce: null pointer");
-    hipLaunchKernelGGL(cd_pair_reduce_kernel, dim3(P + 1, 2 * B), dim3(LT), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(cd_pair_reduce_kernel, dim3(P + 1, 2 * B), dim3(LT), (size_t)3 * 2 * B * (P + 1) * sizeof(float),
+                       (hipStream_t)stream,
                        CdShape{B, S, N, P, NP}, dist_a_full, dist_b_full, dist_a_part, dist_b_part, k, counts, off, ws,
                        counter, terms);
     return ured::launch_status("ured_cd_pair_reduce");
@@ -627,6 +644,8 @@ int ured_contrast_fwd(const float* t, const float* s_all, const long long* src_l
     URED_REQUIRE(n > 0 && n_all >= n && C > 0 && s_off >= 0 && s_off + n <= n_all && n_all <= CT_MAXN,
                  "ured_contrast_fwd: bad sizes (n %d, n_all %d, C %d, s_off %d)", n, n_all, C, s_off);
     URED_REQUIRE(t && s_all && src_labels && inv && lse && ws && counter && loss, "ured_contrast_fwd: null pointer");
+    URED_REQUIRE(C % 4 == 0 && (((uintptr_t)t | (uintptr_t)s_all) & 15) == 0,
+                 "ured_contrast_fwd: C %% 4 == 0 and 16-byte aligned rows required", C);
     ContrastArgs a = contrast_args(n, n_all, C, s_off, scale, t, s_all, src_labels, inv, lse);
     a.part = ws; a.counter = counter; a.loss = loss;
     hipLaunchKernelGGL(contrast_norms_kernel, dim3(n + n_all), dim3(LT), 0, (hipStream_t)stream, a);

@@ -107,9 +107,11 @@ def get_part(cfg, per_point_full, target_labels, x):
     parts = build_parts(target_labels, x, P)
     pp_sorted, sums = part_rows(per_point_full, parts)
     part_mean = sums / parts.counts.reshape(-1, 1).clamp(min=1).float()
-    aabb = part_aabb(parts)                                            # by part slot (rank)
-    param_def = torch.gather(aabb, 1, parts.rank_of_label.clamp(min=0).unsqueeze(-1).expand(-1, -1, 6))
-    param_def = param_def * parts.present.unsqueeze(-1).float()        # indexed by label value (train.py:120)
+    param_def = getattr(parts, "param_def", None)                      # indexed by label value (train.py:120)
+    if param_def is None:
+        aabb = part_aabb(parts)                                        # by part slot (rank)
+        param_def = torch.gather(aabb, 1, parts.rank_of_label.clamp(min=0).unsqueeze(-1).expand(-1, -1, 6))
+        param_def = param_def * parts.present.unsqueeze(-1).float()
     return (part_mean.view(B, P, C), None, ReInput(pp_sorted, part_mean, parts.gid, parts.off),
             parts.mask, parts, param_def)
 

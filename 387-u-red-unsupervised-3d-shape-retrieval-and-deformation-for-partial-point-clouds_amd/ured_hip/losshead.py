@@ -160,7 +160,7 @@ class LossHeadFn(Function):
         d = PointLossDesc(B, N, S, recu.shape[0], NP, mask.shape[0], x.data_ptr(), out.data_ptr(), knn.data_ptr(),
                           res.data_ptr(), rec.data_ptr(), recu.data_ptr(), hi.ptsu.data_ptr(), hi.inv.data_ptr(),
                           mask.data_ptr())
-        pws = torch.empty(3 * ((B * N + 1023) // 1024 + recu.shape[0]), device=dev)
+        pws = torch.empty(3 * ((B * N + 255) // 256 + recu.shape[0]), device=dev)
         _lib.call("ured_point_losses_fwd", ctypes.byref(d), _p(pws), _counter(dev, 1), _p(T[4:]), st)
         # --- contrastive loss (single process: s_all is this rank's s; with several ranks the
         # caller computes it with the gathered codes and passes it in as contrast_ext) ---

@@ -8,6 +8,8 @@ PartBatch     : the ragged per-part view of a target batch that the reference
                 offsets/counts, per-point part id, the mask of present parts.
 build_parts   : computes a PartBatch with device ops only (no host sync).
 """
+import ctypes
+
 import torch
 from torch.autograd import Function
 
@@ -137,7 +139,35 @@ class PartBatch:
         return self.x_sorted.shape[0]
 
 
+_lib.register({"ured_build_parts": [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_void_p] * 13})
+
+
 def build_parts(labels, x, max_parts):
+    """PartBatch of a target batch (engine/train.py:103-136) in ONE HIP launch (ured_build_parts:
+    stable counting sort by label, slot tables, boxes and param_def); build_parts_composed is the
+    same as ~20 torch ops."""
+    if not x.is_cuda:
+        return build_parts_composed(labels, x, max_parts)
+    B, N = labels.shape
+    P = max_parts
+    dev = x.device
+    lab = labels.long().contiguous()
+    xf = x.float().contiguous()
+    L = lambda *s: torch.empty(*s, dtype=torch.int64, device=dev)     # noqa: E731
+    out = dict(x_sorted=torch.empty(B, N, 3, device=dev), perm=L(B, N), inv_perm=L(B, N),
+               gid=torch.empty(B * N, dtype=torch.int32, device=dev), off=torch.empty(B * P + 1, dtype=torch.int32, device=dev),
+               counts=L(B, P), k=L(B), mask=torch.empty(B, P, device=dev), rank_of_label=L(B, P),
+               present=torch.empty(B, P, dtype=torch.bool, device=dev), aabb=torch.empty(B, P, 6, device=dev),
+               param_def=torch.empty(B, P, 6, device=dev))
+    o = out
+    _lib.call("ured_build_parts", _lib.ptr(lab), _lib.ptr(xf), B, N, P, _lib.ptr(o["x_sorted"]), _lib.ptr(o["perm"]),
+              _lib.ptr(o["inv_perm"]), _lib.ptr(o["gid"]), _lib.ptr(o["off"]), _lib.ptr(o["counts"]), _lib.ptr(o["k"]),
+              _lib.ptr(o["mask"]), _lib.ptr(o["rank_of_label"]), _lib.ptr(o["present"]), _lib.ptr(o["aabb"]),
+              _lib.ptr(o["param_def"]), _lib.stream_of(xf))
+    return PartBatch(max_parts=P, **out)
+
+
+def build_parts_composed(labels, x, max_parts):
     B, N = labels.shape
     P = max_parts
     dev = x.device
@@ -164,7 +194,10 @@ def build_parts(labels, x, max_parts):
 
 def part_aabb(parts):
     """[B, P, 6] = (center, half extent) per part slot (compute_aabbox, dataset_utils.py:77-85):
-    one HIP segment min/max launch over the label-sorted points (ured_seg_aabb)."""
+    computed by build_parts, or one HIP segment min/max launch over the label-sorted points
+    (ured_seg_aabb)."""
+    if getattr(parts, "aabb", None) is not None:
+        return parts.aabb
     B, N, _ = parts.x_sorted.shape
     P = parts.max_parts
     flat = parts.x_sorted.reshape(-1, 3)

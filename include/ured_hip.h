@@ -387,6 +387,18 @@ typedef struct {
 int ured_node_bn_bwd(const UredNodeBNBwdDesc* d, void* stream);
 
 
+/* get_part's per-sample bookkeeping (engine/train.py:103-136, compute_aabbox dataset_utils.py:77-85)
+ * in one launch (csrc/parts.hip): labels int64 [B,N] (part ids in [0,P)), x [B,N,3] ->
+ * x_sorted [B,N,3] (points stably sorted by label), perm / inv_perm int64 [B,N], gid int32 [B*N]
+ * (part slot b*P + rank of each sorted point), off int32 [B*P+1] (row offsets of the slots),
+ * counts int64 [B,P], k int64 [B], mask float [B,P], rank_of_label int64 [B,P] (cumsum(present)-1),
+ * present uint8 [B,P], aabb [B,P,6] by slot and param_def [B,P,6] by label value ((center,
+ * half extent), 0 for absent labels). Replaces the per-part Python loop / torch.unique. */
+int ured_build_parts(const long long* labels, const float* x, int B, int N, int P, float* x_sorted,
+                     long long* perm, long long* inv_perm, int* gid, int* off, long long* counts,
+                     long long* k, float* mask, long long* rank_of_label, unsigned char* present,
+                     float* aabb, float* param_def, void* stream);
+
 /* ---------------- loss head (csrc/loss.hip) ---------------- */
 /* compute_cm_loss of the deformed shape `out` [B,S,3] and of its mirror image (x -> -x,
  * get_symmetric) against the same target x [B,N,3] (engine/train.py:288,302 ->

@@ -88,3 +88,27 @@ def test_part_rows_matches_separate_ops(dev, B, N, P, C, kmax):
         outs2 = [t for t, u in ((xs2, use[0]), (sums2, use[1])) if u]
         torch.autograd.backward(outs2, grads)
         assert torch.equal(a.grad, b.grad), (a.grad - b.grad).abs().max().item()
+
+
+@pytest.mark.parametrize("B,N,P,gaps", [(3, 257, 16, True), (16, 2048, 16, False), (2, 5000, 32, True), (1, 7, 16, True)])
+def test_build_parts_kernel_equals_composed(dev, B, N, P, gaps):
+    """ured_build_parts (one launch: stable counting sort, slot tables, boxes, param_def) == the
+    composed torch form (scatter_add / cumsum / stable sort / gathers / ured_seg_aabb) field by
+    field, bitwise; absent labels (gaps) included."""
+    from ured_hip.ops import build_parts, build_parts_composed, part_aabb
+    g = torch.Generator().manual_seed(B * 1000 + N)
+    hi = P if not gaps else P - 3
+    labels = torch.randint(0, hi, (B, N), generator=g)
+    if gaps:
+        labels[labels == 2] = 5                     # label 2 absent everywhere
+    x = torch.randn(B, N, 3, generator=g).to(dev)
+    a = build_parts(labels.to(dev), x, P)
+    c = build_parts_composed(labels.to(dev), x, P)
+    for f in ("x_sorted", "perm", "inv_perm", "gid", "off", "counts", "k", "mask", "rank_of_label", "present"):
+        ta, tc = getattr(a, f), getattr(c, f)
+        assert ta.dtype == tc.dtype and ta.shape == tc.shape, f
+        assert torch.equal(ta, tc), f
+    assert torch.equal(a.aabb, part_aabb(c))
+    pd = torch.gather(part_aabb(c), 1, c.rank_of_label.clamp(min=0).unsqueeze(-1).expand(-1, -1, 6))
+    pd = pd * c.present.unsqueeze(-1).float()
+    assert torch.equal(a.param_def, pd)
