@@ -22,8 +22,8 @@
 //       (the per-term upstream gradients every backward above reads from device memory).
 //
 // Reductions are deterministic: fixed per-thread strides, fixed-shape LDS trees, and the
-// final combine done by the LAST workgroup to finish (an integer arrival counter; the partials
-// are read back at agent scope), in a fixed order, in fp64. The counter is reset by that
+// final combine done by the LAST workgroup to finish (an integer arrival counter; partials
+// stored and read back write-through, see last_arrival), in a fixed order, in fp64. The counter is reset by that
 // workgroup, so a launch leaves it at 0 for the next one (and for HIP-graph replays).
 #include <hip/hip_runtime.h>
 #include "ured_common.h"
@@ -60,24 +60,32 @@ __device__ __forceinline__ float block_max(float v, float* sh) {
     return r;
 }
 
-// Arrival of this workgroup's partials; true in the last workgroup to arrive (which then
-// sees every other workgroup's partials). Thread 0 publishes after a release fence.
+// Arrival of this workgroup's partials; true in the last workgroup to arrive, which may then
+// read every workgroup's partials. The hand-off (MI355X_MICROARCH.md, inter-workgroup
+// visibility, first row of the sc1 table): partials are stored write-through (st_agent: global
+// store sc1), every storing wave waits for its stores (vmcnt(0)) before the workgroup barrier,
+// ONE lane adds to the agent-scope counter, and the workgroup whose add returned the last
+// count reads the partials with sc1 loads (ld_agent) — no cache-flushing fences (__threadfence
+// costs ~3.5 us here). That workgroup resets the counter for the next launch / graph replay.
 __device__ __forceinline__ bool last_arrival(unsigned* counter, unsigned nblocks) {
     __shared__ bool last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();
-        const unsigned prev = atomicAdd(counter, 1u);
+        const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = prev == nblocks - 1;
-        if (last) atomicExch(counter, 0u);      // ready for the next launch / graph replay
+        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (last) __threadfence();
     return last;
 }
 
 __device__ __forceinline__ float ld_agent(const float* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void st_agent(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -163,7 +171,7 @@ __global__ __launch_bounds__(LT) void cd_pair_reduce_kernel(CdShape sh, const fl
         q0 = block_sum(s0, shf);
     }
     const int slot = s * (sh.P + 1) + i;
-    if (t == 0) { part[3 * slot] = q0; part[3 * slot + 1] = q1; part[3 * slot + 2] = q2; }
+    if (t == 0) { st_agent(part + 3 * slot, q0); st_agent(part + 3 * slot + 1, q1); st_agent(part + 3 * slot + 2, q2); }
     if (!last_arrival(counter, gridDim.x * gridDim.y)) return;
     const int units = 2 * sh.B * (sh.P + 1);
     for (int q = t; q < 3 * units; q += LT) stage[q] = ld_agent(part + q);   // independent loads
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(LT) void point_losses_fwd_kernel(PointLossArgs a) {
         q0 = block_sum(l, shf) * w;      // w_u * sum over the part's points
         q1 = msum;
     }
-    if (t == 0) { a.part[3 * blk] = q0; a.part[3 * blk + 1] = q1; a.part[3 * blk + 2] = q2; }
+    if (t == 0) { st_agent(a.part + 3 * blk, q0); st_agent(a.part + 3 * blk + 1, q1); st_agent(a.part + 3 * blk + 2, q2); }
     if (!last_arrival(a.counter, gridDim.x)) return;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     for (int q = t; q < nb1; q += LT) {
@@ -435,8 +443,8 @@ __global__ __launch_bounds__(LT) void contrast_fwd_kernel(ContrastArgs a) {
     if (t == 0) {
         const float l = m + logf(se);
         a.lse[i] = l;
-        a.part[2 * i] = valid ? l - lg[a.s_off + i] : 0.f;
-        a.part[2 * i + 1] = valid ? 1.f : 0.f;
+        st_agent(a.part + 2 * i, valid ? l - lg[a.s_off + i] : 0.f);
+        st_agent(a.part + 2 * i + 1, valid ? 1.f : 0.f);
     }
     if (!last_arrival(a.counter, gridDim.x)) return;
     double s0 = 0.0, s1 = 0.0;
