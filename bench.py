@@ -48,7 +48,8 @@ def workload_cfg(args):
         cfg = json.load(f)
     cfg.update({"batch_size": args.batch, "num_points": args.points, "parts": args.parts,
                 "num_source": args.sources, "device": "cuda", "log_every": 0, "compute_connectivity": False,
-                "flat_adam": os.environ.get("URED_FLAT_ADAM", "1") == "1"})   # A/B knob: torch's Adam
+                "flat_adam": os.environ.get("URED_FLAT_ADAM", "1") == "1",    # A/B knob: torch's Adam
+                "loss_head": os.environ.get("URED_LOSS_HEAD", "1") == "1"})   # A/B knob: composed loss ops
     return cfg
 
 
