@@ -142,11 +142,11 @@ class PartBatch:
 _lib.register({"ured_build_parts": [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_void_p] * 13})
 
 
-def build_parts(labels, x, max_parts):
+def build_parts(labels, x, max_parts, composed=None):
     """PartBatch of a target batch (engine/train.py:103-136) in ONE HIP launch (ured_build_parts:
     stable counting sort by label, slot tables, boxes and param_def); build_parts_composed is the
-    same as ~20 torch ops."""
-    if not x.is_cuda:
+    same as ~20 torch ops (used for CPU tensors, or composed=True)."""
+    if (not x.is_cuda) if composed is None else composed:
         return build_parts_composed(labels, x, max_parts)
     B, N = labels.shape
     P = max_parts

@@ -60,6 +60,12 @@ def main():
     dev = torch.device("cpu")
     db, _ = load_sources(cfg, dev)
     step = TrainStep(cfg, db, dev)
+    # the GPU path's choices (CPU tensors would pick the composed forms)
+    step.loss_head = cfg.get("loss_head", True)
+    import functools
+    import engine.train as et
+    from ured_hip import ops
+    et.build_parts = functools.partial(ops.build_parts, composed=False)
     # the GPU step's optimizer (train_utils/optimizer_dm.py picks it for device parameters only)
     from ured_hip.optim import FlatAdam
     from engine.train import CLIPPED
