@@ -236,7 +236,17 @@ __global__ __launch_bounds__(BN_NT) void node_bn_fwd_kernel(const UredNodeBNDesc
     for (int s = 0; s < d.nsets; ++s) {
         const int r0 = d.off[s], r1 = d.off[s + 1], cnt = r1 - r0;
         float mean, invstd;
-        if (d.training) {
+        if (d.training && d.stats_in) {          // SyncBN: the cross-rank merged statistics
+            const double* st = d.stats_in + (size_t)s * 3 * d.N;
+            const double c = st[nc], mu = st[d.N + nc], var = st[2 * d.N + nc] / fmax(c, 1.0);
+            mean = (float)mu;
+            invstd = (float)(1.0 / sqrt(var + (double)d.eps));
+            if (rl == 0 && cv) {
+                const double unb = c > 1.0 ? var * c / (c - 1.0) : var;
+                d.running_mean[n] = (float)((1.0 - d.momentum) * d.running_mean[n] + d.momentum * mu);
+                d.running_var[n] = (float)((1.0 - d.momentum) * d.running_var[n] + d.momentum * unb);
+            }
+        } else if (d.training) {
             double sum = 0.0;
             for (int m = r0 + rl; m < r1; m += BN_RL) sum += bn_in(d.Y, d.ldy, m, nc, d.relu_in);
             part[rl][cl] = sum;
@@ -258,6 +268,15 @@ __global__ __launch_bounds__(BN_NT) void node_bn_fwd_kernel(const UredNodeBNDesc
             for (int q = 0; q < BN_RL; ++q) m2t += part[q][cl];
             const double var = m2t / (double)max(cnt, 1);
             __syncthreads();
+            if (d.stats_out) {                   // SyncBN: this rank's per-set statistics only
+                if (rl == 0 && cv) {
+                    double* st = d.stats_out + (size_t)s * 3 * d.N;
+                    st[n] = (double)cnt;
+                    st[d.N + n] = mu;
+                    st[2 * d.N + n] = m2t;
+                }
+                continue;
+            }
             mean = (float)mu;
             invstd = (float)(1.0 / sqrt(var + (double)d.eps));
             if (rl == 0 && cv) {
@@ -279,7 +298,7 @@ __global__ __launch_bounds__(BN_NT) void node_bn_fwd_kernel(const UredNodeBNDesc
                 d.act[(long long)m * d.ld_act + n] = bn_in(d.Y, d.ldy, m, n, d.relu_in) * scale + shift;
         __syncthreads();
     }
-    if (d.training && d.num_batches_tracked && blockIdx.x == 0 && threadIdx.x == 0)
+    if (d.training && !d.stats_out && d.num_batches_tracked && blockIdx.x == 0 && threadIdx.x == 0)
         d.num_batches_tracked[0] += d.nsets;
 }
 
@@ -312,11 +331,27 @@ __global__ __launch_bounds__(BN_NT) void node_bn_bwd_kernel(const UredNodeBNBwdD
 #pragma unroll
         for (int q = 0; q < BN_RL; ++q) { sg += pg[q][cl]; sgx += pgx[q][cl]; }
         __syncthreads();
+        if (d.sums_out) {                        // SyncBN: this rank's per-set sums only
+            if (rl == 0 && cv) {
+                double* so = d.sums_out + (size_t)s * 3 * d.N;
+                so[n] = sg;
+                so[d.N + n] = sgx;
+                so[2 * d.N + n] = (double)cnt;
+            }
+            continue;
+        }
         dgam += sgx;
         dbet += sg;
         const float k = gamma * invstd;
-        const float mg = d.training ? (float)(sg / max(cnt, 1)) : 0.f;
-        const float mgx = d.training ? (float)(sgx / max(cnt, 1)) : 0.f;
+        double gsg = sg, gsgx = sgx, gcnt = (double)max(cnt, 1);
+        if (d.sums_in) {                         // SyncBN: the cross-rank sums and count
+            const double* si = d.sums_in + (size_t)s * 3 * d.N;
+            gsg = si[nc];
+            gsgx = si[d.N + nc];
+            gcnt = fmax(si[2 * d.N + nc], 1.0);
+        }
+        const float mg = d.training ? (float)(gsg / gcnt) : 0.f;
+        const float mgx = d.training ? (float)(gsgx / gcnt) : 0.f;
         if (cv)
             for (int m = r0 + rl; m < r1; m += BN_RL) {
                 const float y = d.Y[(long long)m * d.ldy + n];
@@ -327,7 +362,7 @@ __global__ __launch_bounds__(BN_NT) void node_bn_bwd_kernel(const UredNodeBNBwdD
                 d.dY[(long long)m * d.lddy + n] = dx;
             }
     }
-    if (rl == 0 && cv) {
+    if (rl == 0 && cv && !d.sums_out) {
         d.dgamma[n] = d.accumulate ? d.dgamma[n] + (float)dgam : (float)dgam;
         d.dbeta[n] = d.accumulate ? d.dbeta[n] + (float)dbet : (float)dbet;
     }
@@ -395,8 +430,10 @@ int ured_node_bn_fwd(const UredNodeBNDesc* dp, void* stream) {
     URED_REQUIRE(dp, "ured_node_bn_fwd: null descriptor");
     const UredNodeBNDesc& d = *dp;
     URED_REQUIRE(d.nsets >= 1 && d.nsets <= URED_NODE_MAX_SETS && d.N >= 1, "ured_node_bn_fwd: bad sizes");
-    URED_REQUIRE(d.Y && d.gamma && d.beta && d.running_mean && d.running_var && d.mean && d.invstd && d.act,
-                 "ured_node_bn_fwd: null pointer");
+    URED_REQUIRE(d.Y && d.gamma && d.beta && d.running_mean && d.running_var &&
+                 (d.stats_out || (d.mean && d.invstd && d.act)), "ured_node_bn_fwd: null pointer");
+    URED_REQUIRE(!(d.stats_out && d.stats_in), "ured_node_bn_fwd: stats_out and stats_in are exclusive");
+    URED_REQUIRE(d.training || !(d.stats_out || d.stats_in), "ured_node_bn_fwd: SyncBN statistics in eval mode");
     for (int s = 0; s < d.nsets; ++s)
         URED_REQUIRE(d.off[s] <= d.off[s + 1], "ured_node_bn_fwd: set offsets must be non-decreasing");
     hipLaunchKernelGGL(node_bn_fwd_kernel, dim3((d.N + BN_COLS - 1) / BN_COLS), dim3(BN_NT), 0, (hipStream_t)stream, d);
@@ -408,8 +445,9 @@ int ured_node_bn_bwd(const UredNodeBNBwdDesc* dp, void* stream) {
     URED_REQUIRE(dp, "ured_node_bn_bwd: null descriptor");
     const UredNodeBNBwdDesc& d = *dp;
     URED_REQUIRE(d.nsets >= 1 && d.nsets <= URED_NODE_MAX_SETS && d.N >= 1, "ured_node_bn_bwd: bad sizes");
-    URED_REQUIRE(d.G && d.Y && d.gamma && d.mean && d.invstd && d.dY && d.dgamma && d.dbeta,
+    URED_REQUIRE(d.G && d.Y && d.gamma && d.mean && d.invstd && (d.sums_out || (d.dY && d.dgamma && d.dbeta)),
                  "ured_node_bn_bwd: null pointer");
+    URED_REQUIRE(!(d.sums_out && d.sums_in), "ured_node_bn_bwd: sums_out and sums_in are exclusive");
     hipLaunchKernelGGL(node_bn_bwd_kernel, dim3((d.N + BN_COLS - 1) / BN_COLS), dim3(BN_NT), 0, (hipStream_t)stream, d);
     return ured::launch_status("ured_node_bn_bwd");
 }

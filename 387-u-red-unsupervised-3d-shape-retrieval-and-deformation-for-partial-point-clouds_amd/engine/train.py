@@ -132,6 +132,21 @@ class TrainStep:
                               if dev.type == "cuda" and cfg.get("deform_overlap", False) else None)
         # the fused HIP loss head (ured_hip/losshead.py); False: the composed torch + NN-launch form
         self.loss_head = dev.type == "cuda" and cfg.get("loss_head", True) and not cfg.get("stream_overlap", False)
+        # optional SyncBN (ured_hip/syncbn.py): global-batch BN statistics over the ranks
+        import torch.distributed as dist
+        self.sync_bn = bool(cfg.get("sync_bn", False)) and dist.is_initialized() and dist.get_world_size() > 1
+        if self.sync_bn:
+            if dev.type != "cuda":
+                raise NotImplementedError("sync_bn: the HIP BatchNorm path only (a CUDA device)")
+            if self.side_stream is not None or self.deform_stream is not None:
+                raise NotImplementedError("sync_bn: its collectives need one stream order (no stream_overlap / "
+                                          "deform_overlap)")
+        if dev.type == "cuda":       # process-wide: the last step constructed decides
+            from ured_hip import syncbn
+            if self.sync_bn:
+                syncbn.enable()
+            else:
+                syncbn.disable()
 
     def _source_branch(self, uq, src_points, src_sem_f, B, P, expand_rec=True):
         """src_encoder_all + recon_decoder_src (engine/train.py:210-216) -> codes [B*P, C],

@@ -10,4 +10,4 @@
   ops      device-side part building (segment sums, AABBs)
   losshead the step's loss head (chamfer families, contrastive, residual, reconstruction, weighted sum)
 """
-from . import _lib, attn, kernels, losshead, nn, node, ops, optim  # noqa: F401
+from . import _lib, attn, kernels, losshead, nn, node, ops, optim, syncbn  # noqa: F401

@@ -8,7 +8,7 @@ import os
 
 import torch
 
-from . import _lib
+from . import _lib, syncbn
 
 PRO_NONE, PRO_ENC, PRO_RES = 0, 1, 2
 EPI_STORE, EPI_FWD, EPI_BNBWD, EPI_SPLITK = 0, 1, 2, 3
@@ -135,6 +135,10 @@ def bn_fwd_finalize(stat_ws, M, N, gamma, beta, eps, momentum, running_mean, run
     invstd = torch.empty(N, device=dev)
     scale = torch.empty(N, device=dev)
     shift = torch.empty(N, device=dev)
+    if syncbn.active():          # global-batch statistics over the ranks (ured_hip/syncbn.py)
+        syncbn.fwd_finalize(stat_ws, M, N, gamma, beta, eps, momentum, running_mean, running_var, rw,
+                            num_batches_tracked, (mean, invstd, scale, shift))
+        return BNState(mean, invstd, scale, shift)
     _lib.call("ured_bn_fwd_finalize", _p(stat_ws), int(M), int(N), _p(gamma), _p(beta), float(eps), float(momentum),
               _p(running_mean), _p(running_var), _p(mean), _p(invstd), _p(scale), _p(shift), *_rw(rw),
               _p(num_batches_tracked), _lib.stream_of(stat_ws))
@@ -150,6 +154,9 @@ def bn_eval_state(gamma, beta, running_mean, running_var, eps):
 def bn_bwd_finalize(bwd_ws, M, N, gamma, invstd, dgamma, dbeta, rw=None):
     dev = bwd_ws.device
     ca, cb, cc = (torch.empty(N, device=dev) for _ in range(3))
+    if syncbn.active():
+        syncbn.bwd_finalize(bwd_ws, M, N, gamma, invstd, dgamma, dbeta, rw, (ca, cb, cc))
+        return ca, cb, cc
     _lib.call("ured_bn_bwd_finalize", _p(bwd_ws), int(M), int(N), _p(gamma), _p(invstd), _p(dgamma), _p(dbeta), 0,
               _p(ca), _p(cb), _p(cc), *_rw(rw), _lib.stream_of(bwd_ws))
     return ca, cb, cc

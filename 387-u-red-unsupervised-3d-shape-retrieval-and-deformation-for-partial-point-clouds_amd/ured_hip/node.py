@@ -24,7 +24,7 @@ import ctypes
 import torch
 from torch.autograd import Function
 
-from . import _lib
+from . import _lib, syncbn
 from . import kernels as K
 from .optim import grad_buffer, grad_slot
 
@@ -54,7 +54,8 @@ class NodeBNDesc(ctypes.Structure):
                 ("running_mean", _P), ("running_var", _P), ("num_batches_tracked", _P),
                 ("momentum", _F), ("eps", _F),
                 ("mean", _P), ("invstd", _P),
-                ("act", _P), ("ld_act", _LL)]
+                ("act", _P), ("ld_act", _LL),
+                ("stats_out", _P), ("stats_in", _P)]
 
 
 class NodeBNBwdDesc(ctypes.Structure):
@@ -63,7 +64,8 @@ class NodeBNBwdDesc(ctypes.Structure):
                 ("Y", _P), ("ldy", _LL), ("relu_in", _I), ("training", _I),
                 ("gamma", _P), ("mean", _P), ("invstd", _P),
                 ("dY", _P), ("lddy", _LL),
-                ("dgamma", _P), ("dbeta", _P), ("accumulate", _I)]
+                ("dgamma", _P), ("dbeta", _P), ("accumulate", _I),
+                ("sums_out", _P), ("sums_in", _P)]
 
 
 MAX_JOBS = 6
@@ -216,7 +218,15 @@ def bn_fwd(Y, bnm, off, training, relu_in=True):
     d.eps = bnm.eps
     d.mean, d.invstd = mean.data_ptr(), invstd.data_ptr()
     d.act, d.ld_act = act.data_ptr(), act.stride(0)
-    _lib.call("ured_node_bn_fwd", ctypes.byref(d), _lib.stream_of(Y))
+    stream = _lib.stream_of(Y)
+    if training and syncbn.active():
+        # SyncBN: this rank's per-set (count, mean, M2) -> merged over the ranks -> normalise
+        local = torch.empty(nsets, 3, N, dtype=torch.float64, device=Y.device)
+        d.stats_out = local.data_ptr()
+        _lib.call("ured_node_bn_fwd", ctypes.byref(d), stream)
+        glob = syncbn.merge_stats(local)
+        d.stats_out, d.stats_in = None, glob.data_ptr()
+    _lib.call("ured_node_bn_fwd", ctypes.byref(d), stream)
     return act, mean, invstd
 
 
@@ -234,7 +244,15 @@ def bn_bwd(G, Y, gamma, mean, invstd, off, training, relu_in=True, dgamma=None, 
     d.gamma, d.mean, d.invstd = gamma.data_ptr(), mean.data_ptr(), invstd.data_ptr()
     d.dY, d.lddy = dY.data_ptr(), dY.stride(0)
     d.dgamma, d.dbeta, d.accumulate = dgamma.data_ptr(), dbeta.data_ptr(), int(bool(accumulate))
-    _lib.call("ured_node_bn_bwd", ctypes.byref(d), _lib.stream_of(Y))
+    stream = _lib.stream_of(Y)
+    if training and syncbn.active():
+        # SyncBN: the input gradient from the ranks' summed (sum g, sum g*xhat, count)
+        local = torch.empty(nsets, 3, N, dtype=torch.float64, device=Y.device)
+        d.sums_out = local.data_ptr()
+        _lib.call("ured_node_bn_bwd", ctypes.byref(d), stream)
+        glob = syncbn.sum_over_ranks(local)
+        d.sums_out, d.sums_in = None, glob.data_ptr()
+    _lib.call("ured_node_bn_bwd", ctypes.byref(d), stream)
     return dY, dgamma, dbeta
 
 

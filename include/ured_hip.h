@@ -40,7 +40,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 4   /* 4: BN partial workspaces laid out [2][N][blocks]; ured_part_rows_bwd */
+#define URED_ABI_VERSION 5   /* 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
@@ -264,6 +264,25 @@ int ured_bn_bwd_finalize(const float* bwd_ws, int M, int N, const float* gamma, 
                          float* coef_a, float* coef_b, float* coef_c,
                          const float* group_w, int group_rows, void* stream);
 
+/* ---- SyncBN (optional, cfg["sync_bn"]; csrc/syncbn.hip): the two finalizes above split
+ * around a cross-rank exchange of fp64 per-column statistics, torch SyncBatchNorm semantics.
+ * ured_bn_stats: the Chan merge of ured_bn_fwd_finalize stopped before normalising:
+ *   out [3][N] = (weighted count, mean, M2) of this rank's rows.
+ * ured_bn_finalize_stats: ured_bn_fwd_finalize's outputs from merged stats [3][N].
+ * ured_bn_bwd_sums: out [3][N] = (sum g, sum g*xhat, weighted count) of this rank.
+ * ured_bn_bwd_finalize_sums: dbeta / dgamma from `local` (written or added), the
+ *   ured_bn_bwd_apply coefficients from `global` (the all-reduced sums and count). */
+int ured_bn_stats(const float* stat_ws, int M, int N, const float* group_w, int group_rows, double* out,
+                  void* stream);
+int ured_bn_finalize_stats(const double* stats, int N, const float* gamma, const float* beta, float eps,
+                           float momentum, float* running_mean, float* running_var, float* mean, float* invstd,
+                           float* scale, float* shift, long long* num_batches_tracked, void* stream);
+int ured_bn_bwd_sums(const float* bwd_ws, int M, int N, const float* group_w, int group_rows, double* out,
+                     void* stream);
+int ured_bn_bwd_finalize_sums(const double* local, const double* global, int N, const float* gamma,
+                              const float* invstd, float* dgamma, float* dbeta, int accumulate, float* coef_a,
+                              float* coef_b, float* coef_c, void* stream);
+
 /* dY[m][n] = coef_a*g + coef_b*(p-mean) + coef_c with p = Y (ENC) or relu(Y) (RES, then
  * times (Y > 0)). Also writes per-128-row column partial sums of dY to colsum_ws[blk][N].
  * With group_w, G holds the multiplicity-summed gradient of each stored row and the
@@ -361,7 +380,11 @@ int ured_node_gemm_batch(const UredNodeGemmDesc* const* d, int n, void* stream);
  * x = relu_in ? max(Y, 0) : Y. training: per-set batch mean / biased variance (fp64 sums),
  * running stats updated per set in order (unbiased variance, momentum), num_batches_tracked
  * (nullable) += nsets; eval: running stats. Writes mean/invstd [nsets][N] and
- * act[m*ld_act+n] = (x - mean) * invstd * gamma + beta. */
+ * act[m*ld_act+n] = (x - mean) * invstd * gamma + beta.
+ * SyncBN (training only): stats_out non-NULL -> ONLY write each set's local fp64 (count, mean,
+ * M2) to stats_out [nsets][3][N] and return (nothing else is written); stats_in non-NULL -> use
+ * those (cross-rank merged) per-set statistics instead of this call's rows (running stats
+ * updated with the merged count's unbiased variance). */
 #define URED_NODE_MAX_SETS 4
 typedef struct {
     int N, nsets, off[URED_NODE_MAX_SETS + 1];
@@ -371,11 +394,15 @@ typedef struct {
     float momentum, eps;
     float* mean; float* invstd;
     float* act; long long ld_act;
+    double* stats_out; const double* stats_in;
 } UredNodeBNDesc;
 int ured_node_bn_fwd(const UredNodeBNDesc* d, void* stream);
 
 /* Backward of ured_node_bn_fwd: G = d loss / d act -> dY (through the ReLU when relu_in),
- * dgamma / dbeta summed over the sets (written, or added if accumulate). */
+ * dgamma / dbeta summed over the sets (written, or added if accumulate).
+ * SyncBN: sums_out non-NULL -> ONLY write each set's local fp64 (sum g, sum g*xhat, count) to
+ * sums_out [nsets][3][N] and return; sums_in non-NULL -> the input gradient uses those
+ * (cross-rank summed) sums and counts, dgamma / dbeta stay this rank's local sums. */
 typedef struct {
     int N, nsets, off[URED_NODE_MAX_SETS + 1];
     const float* G; long long ldg;
@@ -383,6 +410,7 @@ typedef struct {
     const float* gamma; const float* mean; const float* invstd;
     float* dY; long long lddy;
     float* dgamma; float* dbeta; int accumulate;
+    double* sums_out; const double* sums_in;
 } UredNodeBNBwdDesc;
 int ured_node_bn_bwd(const UredNodeBNBwdDesc* d, void* stream);
 
