@@ -37,7 +37,7 @@ REFERENCE_UNREAD = {
 EXTRA = {
     "synthetic", "seed", "num_points", "parts", "num_targets", "iters_per_epoch", "pseudo_labels",
     "unique_sources", "flat_adam", "fused_adam", "cuda_graph", "stream_overlap", "deform_overlap",
-    "log_every", "compute_connectivity", "differentiable_gather", "sync_bn",
+    "log_every", "compute_connectivity", "differentiable_gather", "sync_bn", "loss_head", "dist_backend",
 }
 
 TRAIN_REQUIRED = ("source_latent_dim", "target_latent_dim", "sem_latent_dim", "MAX_NUM_PARTS", "device",

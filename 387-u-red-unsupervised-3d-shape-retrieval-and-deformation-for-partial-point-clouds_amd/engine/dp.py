@@ -6,14 +6,16 @@ loss/contrast_loss.py keeps. This adds the standard DP step: each rank runs the 
 own shard of samples (weak scaling, bs per GPU fixed), and the gradients of every parameter
 that has one this step are averaged (stn1/stn2/part_encoding never get one and are skipped: the
 find_unused_parameters equivalent; re_residual_net_full joins once the residual loss switches
-on). BatchNorm uses per-rank batch statistics (what DDP does without SyncBN).
+on). BatchNorm uses per-rank batch statistics (what DDP does without SyncBN; cfg["sync_bn"]:
+global ones, ured_hip/syncbn.py). The constructor broadcasts rank 0's parameters and buffers.
 
 With FlatAdam (the default optimizer on the GPU) the gradients are reduced in place in its flat
 gradient buffer, in buckets of ~bucket_mb MB that are issued DURING backward:
   * the first step learns the order in which backward produces the gradients (post-accumulate
     hooks) and FlatAdam lays its flat buffers out in that order, so a bucket is one contiguous
     range that fills early; the (offset, size, active) layout is checked equal on every rank
-    once (an all-reduce of its hash), so that every rank reduces the same ranges;
+    on the first step and whenever the set of parameters with a gradient changes (an all-reduce
+    of its hash), so that every rank reduces the same ranges;
   * from the second step on, each parameter's post-accumulate hook counts its bucket down;
     a full bucket's gradients are copied into their flat views (one multi-tensor copy) and its
     all_reduce is issued asynchronously (RCCL runs it on its own stream after the copy, while
@@ -110,7 +112,7 @@ class FlatGradReducer:
         self._next = 0
         self._armed = False
         self._step_armed = False
-        self._checked = False
+        self._checked = None                # the active set whose layout was last checked across ranks
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params] if overlap else []
 
     # hooks run on the autograd thread, in gradient-production order
@@ -171,7 +173,7 @@ class FlatGradReducer:
         if int(t[0]) != h or -int(t[1]) != h:
             raise RuntimeError("data-parallel: the flat gradient layout differs between ranks "
                                "(different parameter sets with gradients); refusing to all-reduce")
-        self._checked = True
+        self._checked = self.opt._active
 
     @property
     def num_buckets(self):
@@ -195,7 +197,10 @@ class FlatGradReducer:
         if opt.flat_param is None and self._arrival:
             opt.layout_order = list(self._arrival)        # first step: backward's order
         active = opt.prepare()
-        if not self._checked:
+        if self._checked != active:
+            # first step, or the set of parameters with a gradient changed (e.g. the residual net
+            # joining): every rank must reduce the same ranges — checked again (one tiny
+            # all_reduce, only when the set changes)
             self._check_layout()
         if not armed or not any(b.launched for b in self._fb):
             # first step (overlap off, a captured step, or no bucket filled): all after backward
@@ -225,6 +230,8 @@ class DataParallelStep(TrainStep):
     def __init__(self, cfg, db, device, bucket_mb=25.0, overlap=None):
         super().__init__(cfg, db, device)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        if self.world > 1:
+            self.broadcast_state()
         params = []
         for name in CLIPPED:
             params += [p for p in self.models[name].parameters() if p.requires_grad]
@@ -234,6 +241,14 @@ class DataParallelStep(TrainStep):
         overlap = (self.world > 1) if overlap is None else bool(overlap)
         self.reducer = (FlatGradReducer(self.optimizer, params, self.world, self.bucket_elems, overlap)
                         if self.world > 1 and hasattr(self.optimizer, "prepare") else None)
+
+    def broadcast_state(self, src=0):
+        """Every rank starts from rank src's parameters and buffers (as DDP's constructor does:
+        each process initialised its modules from its own RNG stream)."""
+        with torch.no_grad():
+            for name in sorted(self.models):
+                for t in list(self.models[name].parameters()) + list(self.models[name].buffers()):
+                    dist.broadcast(t.data, src)
 
     def step(self, batch, epoch=0):
         self.optimizer.zero_grad(set_to_none=True)

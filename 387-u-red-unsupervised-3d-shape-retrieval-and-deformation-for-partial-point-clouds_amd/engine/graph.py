@@ -24,12 +24,25 @@ changes (re_residual_net_full joins): every graph, the update graph and the pers
 gradients are dropped and the next step runs eagerly again.
 
 Same kernels, same arithmetic as the eager step: a replay is bit-identical to an eager step on
-the same state and batch. With world > 1 the forward contains the contrastive loss's
-all_gather; graph mode is then opt-in (bench --graph-dp), the default keeps the eager path.
+the same state and batch.
+
+Data parallel (world > 1): the forward contains collectives — the contrastive loss's all_gather
+of the source codes and, with SyncBN, every BN layer's statistics exchange. No collective is
+captured: the fwd_bwd region is captured as a chain of graphs split at each collective
+(ured_hip/collective.py SegmentedCapture), and a replay runs segment, collective, segment, ...
+with the collectives issued eagerly on the segments' static buffers (any backend, gloo
+included). The gradients of the parameters that torch (not a HIP layer) produces are copied
+into their flat-gradient views INSIDE the last segment, so the gradient all-reduce that follows
+the replay (reduce_gradients, eager) reads every gradient of this step and the update graph
+contains no copy that could overwrite the averaged values.
 """
 from collections import OrderedDict
 
+import gc
+
 import torch
+
+from ured_hip.collective import SegmentedCapture
 
 
 def _clone_batch(batch):
@@ -45,6 +58,12 @@ def _detached(T):
 
 class GraphedStep:
     def __init__(self, inner, example_batch=None, warmup=0, max_graphs=6):
+        import torch.distributed as dist
+        if (dist.is_initialized() and dist.get_world_size() > 1
+                and (getattr(inner, "side_stream", None) is not None or getattr(inner, "deform_stream", None) is not None)):
+            # a capture segment must end with every forked stream joined; the side-stream forms
+            # issue the contrastive all_gather on their side stream
+            raise NotImplementedError("graph replay with world > 1: not with stream_overlap / deform_overlap")
         self.inner = inner
         self.max_graphs = max_graphs
         self.graphs = OrderedDict()       # key -> (static batch, graph, loss dict)
@@ -66,6 +85,17 @@ class GraphedStep:
     @property
     def optimizer(self):
         return self.inner.optimizer
+
+    @property
+    def scheduler(self):
+        return self.inner.scheduler
+
+    @property
+    def cfg(self):
+        return self.inner.cfg
+
+    def state_dict(self):
+        return self.inner.state_dict()
 
     def gate(self, epoch):
         cfg = self.inner.cfg
@@ -102,15 +132,33 @@ class GraphedStep:
     def _capture(self, key, batch, epoch):
         static = _clone_batch(batch)
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
+        gc.collect()
         flat = self._flat()
         if flat:
             self.inner.optimizer.zero_grad(set_to_none=True)
-        with torch.cuda.graph(g):
-            if not flat:
-                torch._foreach_zero_(self.grads)
-            loss, T = self.inner.forward(static, epoch)
-            loss.backward()
+        cap = SegmentedCapture()
+        stream = torch.cuda.Stream()
+        stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream):
+            cap.begin()
+            try:
+                if not flat:
+                    torch._foreach_zero_(self.grads)
+                loss, T = self.inner.forward(static, epoch)
+                loss.backward()
+                if flat:
+                    # torch-produced gradients into their flat views, inside the captured region
+                    self.inner.optimizer.gather_grads()
+            except BaseException:
+                cap.abort()
+                raise
+            cap.end()
+        torch.cuda.current_stream().wait_stream(stream)
+        if flat:
+            opt = self.inner.optimizer
+            for p, v, a in zip(opt.params_all, opt._gviews, opt._active):
+                if a and p.grad.data_ptr() != v.data_ptr():
+                    raise RuntimeError("graph capture: a gradient is not its flat-gradient view")
         T = _detached(T)
         del loss
         if self.g_update is None:
@@ -118,7 +166,7 @@ class GraphedStep:
             with torch.cuda.graph(gu):
                 self.inner.clip_and_step()
             self.g_update = gu
-        self.graphs[key] = (static, g, T)
+        self.graphs[key] = (static, cap, T)
         while len(self.graphs) > self.max_graphs:
             self.graphs.popitem(last=False)
 
@@ -142,10 +190,10 @@ class GraphedStep:
             self._capture(k, batch, epoch)
             return T
         self.graphs.move_to_end(k)
-        static, g, T = ent
+        static, cap, T = ent
         for name, v in static.items():
             v.copy_(batch[name], non_blocking=True)
-        g.replay()
+        cap.replay()                         # segments, and the collectives between them
         self.inner.reduce_gradients()
         sync = getattr(self.inner.optimizer, "sync_lr", None)
         if sync is not None:                 # FlatAdam reads lr from a device scalar

@@ -556,19 +556,27 @@ def save_model(model, start, epoch, cfg):
 
 def init_distributed(cfg):
     """torchrun environment -> (rank, world, device). One process per GPU; RCCL ("nccl") on
-    ROCm devices, gloo on CPU. Single process: (0, 1, cfg["device"])."""
+    ROCm devices, gloo on CPU; cfg["dist_backend"] overrides the backend (gloo on GPUs: the
+    multi-rank tests run every rank on the one GPU of a test box, local rank modulo the device
+    count). Single process: (0, 1, cfg["device"])."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return 0, 1, cfg["device"]
     import torch.distributed as dist
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if str(cfg["device"]).startswith("cuda"):
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
-        dist.init_process_group("nccl", device_id=device)
+        backend = cfg.get("dist_backend", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            device = torch.device("cuda", local)
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            device = torch.device("cuda", local % torch.cuda.device_count())
+            torch.cuda.set_device(device)
+            dist.init_process_group(backend)
     else:
         device = torch.device(cfg["device"])
-        dist.init_process_group("gloo")
+        dist.init_process_group(cfg.get("dist_backend", "gloo"))
     return dist.get_rank(), dist.get_world_size(), device
 
 
@@ -581,6 +589,11 @@ def main(cfg):
         trainer = DataParallelStep(cfg, db, device)
     else:
         trainer = TrainStep(cfg, db, device)
+    if cfg.get("cuda_graph", False) and torch.device(device).type == "cuda":
+        # the step replayed as HIP graphs (engine/graph.py); the loaders pad the distinct-source
+        # count to a multiple of 8 so that few graphs serve all batches
+        from engine.graph import GraphedStep
+        trainer = GraphedStep(trainer)
     # each rank draws its own shard of samples (weak scaling: batch_size per GPU)
     loader = make_loader(cfg, db, device, seed=int(cfg.get("seed", 0)) + 7919 * rank, dist_src=dist_src)
     writer = _ScalarLog(cfg["log_path"]) if rank == 0 else None

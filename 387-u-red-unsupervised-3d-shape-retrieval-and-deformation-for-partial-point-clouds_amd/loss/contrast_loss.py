@@ -29,10 +29,13 @@ def all_gather_batch(tensors, differentiable=False):
     world = get_world_size()
     if world == 1:
         return tensors
+    from ured_hip import collective
     out = []
     for t in tensors:
         bufs = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(bufs, t.contiguous())
+        tc = t.contiguous()
+        # eager, or between two segments of a captured step (ured_hip/collective.py)
+        collective.run(lambda bufs=bufs, tc=tc: dist.all_gather(bufs, tc))
         if differentiable:
             bufs[get_rank()] = t
         out.append(torch.cat(bufs, 0))
@@ -51,7 +54,9 @@ def compute_contrast_loss_loss(tgt_part_f, src_f, src_labels, differentiable_gat
     labels = (n * get_rank() + torch.arange(n, device=t.device)).masked_fill_(src_labels.reshape(n).to(t.device) == -1, -1)
     t_e = F.normalize(t, dim=-1, p=2)
     s_e = F.normalize(s, dim=-1, p=2)
-    _, s_all = all_gather_batch([t_e, s_e], differentiable=differentiable_gather)
+    # the reference gathers [t_e, s_e] and discards the gathered t_e (contrast_loss.py:35-58):
+    # only the source codes are gathered here (same logits, one collective fewer)
+    (s_all,) = all_gather_batch([s_e], differentiable=differentiable_gather)
     scale = _SCALE32                    # exp(logit scale) rounded to fp32 once, as the fp32 tensor exp would
     if t_e.is_cuda:
         # logits t_e s_all^T on the node GEMM (csrc/node.hip): forward and both backward GEMMs

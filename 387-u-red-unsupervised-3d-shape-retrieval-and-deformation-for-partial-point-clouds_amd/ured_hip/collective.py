@@ -1,0 +1,84 @@
+"""Collectives inside the training step, and HIP-graph capture around them.
+
+The data-parallel step issues collectives in the middle of its forward / backward: the
+contrastive loss's all_gather of the source codes (loss/contrast_loss.py) and, with SyncBN, the
+per-layer statistics exchanges (ured_hip/syncbn.py). Every such call goes through run(). Eagerly
+it just issues the collective. While engine/graph.py captures the step, run() instead closes
+the captured segment, records the collective and opens the next segment: a replay is then
+segment 0, collective 0, segment 1, ... — the collectives run eagerly between replays on
+static buffers (no collective is ever captured into a graph, so the capture works with any
+process-group backend, gloo included).
+"""
+
+_split = None
+
+
+def run(fn):
+    """Issue the collective `fn()` (no arguments, no return value; in- and outputs are tensors it
+    closes over, at fixed addresses while a graph replays them)."""
+    if _split is None:
+        fn()
+    else:
+        _split(fn)
+
+
+class SegmentedCapture:
+    """Capture a region as a chain of HIP graphs split at run() calls (engine/graph.py).
+
+        cap = SegmentedCapture(pool)
+        with torch.cuda.stream(s):
+            cap.begin(); <forward / backward>; cap.end()
+        cap.replay()
+    """
+
+    def __init__(self, pool=None):
+        import torch
+        self._torch = torch
+        self.pool = pool if pool is not None else torch.cuda.graph_pool_handle()
+        self.graphs, self.collectives = [], []
+        self._g = None
+
+    def _open(self):
+        # relaxed: a split inside backward closes the segment on the autograd engine's thread
+        # and opens the next one there; the main thread closes the last one
+        self._g = self._torch.cuda.CUDAGraph()
+        self._g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
+
+    def _close(self):
+        self._g.capture_end()
+        self.graphs.append(self._g)
+        self._g = None
+
+    def _split_at(self, fn):
+        self._close()
+        self.collectives.append(fn)
+        self._open()
+
+    def begin(self):
+        global _split
+        if _split is not None:
+            raise RuntimeError("nested segmented capture")
+        self._open()
+        _split = self._split_at
+
+    def end(self):
+        global _split
+        _split = None
+        self._close()
+
+    def abort(self):
+        """After an exception inside the captured region: leave capture mode."""
+        global _split
+        _split = None
+        if self._g is not None:
+            try:
+                self._g.capture_end()
+            except Exception:
+                pass
+            self._g = None
+
+    def replay(self):
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.collectives):
+                self.collectives[i]()

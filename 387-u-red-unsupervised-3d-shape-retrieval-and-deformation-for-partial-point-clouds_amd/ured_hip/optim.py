@@ -80,7 +80,12 @@ def grad_slot(t):
     that input, so autograd has no second gradient to add: either p.grad already is the view, or
     AccumulateGrad has not run yet and will adopt (or copy) the view after this backward's kernels
     on the same stream. Every other case (no flat layout, gradients kept across backward calls, a
-    double-backward) gets a fresh tensor and accumulate=False: autograd's usual accumulation."""
+    double-backward) gets a fresh tensor and accumulate=False: autograd's usual accumulation.
+    Contract of the accumulate path: EVERY producer of that parameter's gradient in the backward
+    goes through grad_slot / grad_buffer. A non-HIP producer arriving between two HIP uses would
+    make autograd sum out of place, and the later in-kernel add would land in a tensor autograd
+    no longer holds; gather_grads() checks for exactly that (p.grad must be the view of an
+    accumulated slot) and raises instead of losing the contribution."""
     sv = _slot_view(t)
     if sv is not None and not torch.is_grad_enabled():
         p, view, opt = sv
@@ -88,6 +93,7 @@ def grad_slot(t):
             p._ured_gclaim = opt._gen
             return view, False
         if getattr(p, "_ured_gclaim", None) == opt._gen and (p.grad is None or p.grad.data_ptr() == view.data_ptr()):
+            p._ured_gacc = opt._gen
             return view, True
     return torch.empty(t.shape, device=t.device), False
 
@@ -250,6 +256,9 @@ class FlatAdam(torch.optim.Optimizer):
                 continue
             g = p.grad
             if g.data_ptr() != v.data_ptr():
+                if getattr(p, "_ured_gacc", None) == self._gen:
+                    raise RuntimeError("FlatAdam: a gradient accumulated in place into its flat view (grad_slot) "
+                                       "was replaced by autograd (a producer outside grad_slot); it would be lost")
                 dst.append(v)
                 src.append(g)
             p.grad = v

@@ -13,7 +13,8 @@ SyncBatchNorm semantics (torch/nn/modules/_functions.py):
   backward: the fp64 sums (sum g, sum g*xhat, count) are all-reduced; the input gradient uses
             the global sums, dgamma / dbeta are the rank's local sums (the gradient all-reduce
             of the DP step then averages them, as DDP does with SyncBatchNorm).
-Collectives are issued in the same order on every rank (the forward / backward layer order).
+Collectives are issued in the same order on every rank (the forward / backward layer order),
+through ured_hip/collective.run (so a captured step replays them between graph segments).
 The state is process-wide: TrainStep enables it for its process group when cfg["sync_bn"] and
 world > 1 (engine/train.py), and a layer in eval mode never synchronises.
 """
@@ -22,7 +23,7 @@ import ctypes
 import torch
 import torch.distributed as dist
 
-from . import _lib
+from . import _lib, collective
 
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _lib.register({
@@ -56,7 +57,8 @@ def merge_stats(local):
     merged in rank order (the same arithmetic on every rank)."""
     local = local.contiguous()
     parts = [torch.empty_like(local) for _ in range(_state["world"])]
-    dist.all_gather(parts, local, group=_state["group"])
+    group = _state["group"]
+    collective.run(lambda: dist.all_gather(parts, local, group=group))
     st = torch.stack(parts)                               # [world, ..., 3, N]
     c, mu, m2 = st.select(-2, 0), st.select(-2, 1), st.select(-2, 2)
     C = c.sum(0)
@@ -68,7 +70,8 @@ def merge_stats(local):
 def sum_over_ranks(local):
     """local fp64 sums -> their sum over the ranks (a new tensor; `local` is kept)."""
     g = local.clone()
-    dist.all_reduce(g, op=dist.ReduceOp.SUM, group=_state["group"])
+    group = _state["group"]
+    collective.run(lambda: dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group))
     return g
 
 

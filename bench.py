@@ -499,9 +499,10 @@ def main():
                     help="issue the step eagerly (Python + ctypes launches, ~700 per step) instead of replaying it "
                          "as HIP graphs. Graph replay (engine/graph.py, bitwise equal to eager) is the default at "
                          "N=1: the GPU-side step is ~16 ms, and on a slow host the eager launch stream cannot keep "
-                         "up (51 vs 63 it/s measured on one box); N > 1 replays only with --graph-dp")
+                         "up (51 vs 63 it/s measured on one box). N > 1 replays too: the captured step is split "
+                         "at its collectives, which run eagerly between the graph segments (engine/graph.py)")
     ap.add_argument("--graph", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old commands
-    ap.add_argument("--graph-dp", action="store_true", help="HIP-graph replay also when N > 1")
+    ap.add_argument("--graph-dp", action="store_true", help=argparse.SUPPRESS)   # graph replay is the N > 1 default
     ap.add_argument("--graph-bucket", type=int, default=1,
                     help="graph mode: pad the distinct-source-part count to a multiple of this (one graph per count)")
     ap.add_argument("--overlap", action="store_true",
@@ -549,7 +550,7 @@ def main():
     from dataset import synthetic
 
     cfg = workload_cfg(args)
-    use_graph = not args.eager and (world == 1 or args.graph_dp)
+    use_graph = not args.eager
     cfg["cuda_graph"] = use_graph
     cfg["stream_overlap"] = args.overlap
     cfg["deform_overlap"] = args.deform_overlap
