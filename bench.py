@@ -34,12 +34,12 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X fp32 (vector = matrix) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARY = "r2o_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
+PMC_SUMMARY = "r3g_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
 # rocprofv3 --kernel-trace --stats of the headline command (tools/prof_step.sh), restricted to its timed
 # steps: the dominant kernel's average duration there is what roofline.achieved / frac are computed from
-PROF_STATS = "r2o_step_kernel_stats.csv"
-CLOCK_SUMMARY = "r2o_clock_summary.json"   # GRBM_GUI_ACTIVE pass (tools/gpu_clock_sq.sh): clock held per kernel
-SQ_SUMMARY = "r2o_sq_summary.json"         # SQ pass (tools/gpu_clock_sq.sh): MFMA-busy cycles per kernel
+PROF_STATS = "r3g_step_kernel_stats.csv"
+CLOCK_SUMMARY = "r3g_clock_summary.json"   # GRBM_GUI_ACTIVE pass (tools/gpu_clock_sq.sh): clock held per kernel
+SQ_SUMMARY = "r3g_sq_summary.json"         # SQ pass (tools/gpu_clock_sq.sh): MFMA-busy cycles per kernel
 NOMINAL_GHZ = 2.4
 
 
@@ -439,7 +439,7 @@ def _free_port():
 def launch_ranks(args):
     """`--gpus N` without torch.distributed.run: start the N ranks as a child process (nothing in
     this process has initialised the GPU: torch.cuda.device_count() does not on this image)."""
-    if not args.cpu_dry_run:
+    if not args.cpu_dry_run and args.dist_backend == "nccl":
         n = torch.cuda.device_count()
         if n < args.gpus:
             print(f"bench.py: --gpus {args.gpus} but only {n} GPU(s) visible", file=sys.stderr)
@@ -523,6 +523,9 @@ def main():
                     help="skip the extra timed run that takes every batch from the pseudo-label loader "
                          "and uploads it inside the timed loop")
     ap.add_argument("--cpu-dry-run", action="store_true", help=argparse.SUPPRESS)
+    # gloo: every rank on GPU (local rank mod the device count) — the rehearsal of the N > 1 code
+    # path on a one-GPU box (tests); its rates mean nothing
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -533,8 +536,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local %= torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
         world, rank = dist.get_world_size(), dist.get_rank()
     if world != args.gpus and rank == 0:
         print(f"bench.py: running {world} rank(s) (--gpus {args.gpus})", file=sys.stderr)
