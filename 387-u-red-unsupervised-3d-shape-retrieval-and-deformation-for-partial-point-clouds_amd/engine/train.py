@@ -142,7 +142,11 @@ class TrainStep:
                 raise NotImplementedError("sync_bn: its collectives need one stream order (no stream_overlap / "
                                           "deform_overlap)")
         if dev.type == "cuda":       # process-wide: the last step constructed decides
-            from ured_hip import syncbn
+            from ured_hip import sidework, syncbn
+            if self.side_stream is not None or self.deform_stream is not None:
+                # the chains' weight-gradient side stream is not nested inside these side streams
+                # (a graph capture of that nesting crashed the HIP runtime on MI355X)
+                sidework.MODE = 0
             if self.sync_bn:
                 syncbn.enable()
             else:

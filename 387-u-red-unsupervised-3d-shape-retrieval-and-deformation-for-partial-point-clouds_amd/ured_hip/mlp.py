@@ -18,7 +18,9 @@ from torch.autograd import Function
 
 from . import _lib
 from . import kernels as K
+from . import syncbn
 from .optim import grad_buffer
+from .sidework import SideWork
 
 BN_EPS = 1e-5
 
@@ -143,20 +145,23 @@ class PointEncoderFn(Function):
         W8, fcW = params[28].reshape(params[28].shape[0], -1), params[30]
         C = W8.shape[0]
         grads = [None] * 32
+        sw = _side_work(dev)
         dcode = torch.zeros(G, C, device=dev) if dcode is None else dcode.contiguous()
         dpp = torch.zeros(M, C, device=dev) if dpp is None else dpp.contiguous()
         # fc: code = pooled @ fcW^T + fcb
         NP = pooled.shape[1]
         dpool = torch.empty(G, NP, device=dev)
         K.gemm(G, NP, C, dcode, C, fcW, NP, dpool, NP, b_kmajor=True)
-        dfcW = grad_buffer(fcW)
-        K.wgrad(dcode, C, pooled, NP, C, NP, G, dfcW, NP)
-        grads[30], grads[31] = dfcW, K.colsum(dcode, out=grad_buffer(params[31]))
+        dfcW, dfcb = grad_buffer(fcW), grad_buffer(params[31])
+        K.wgrad(dcode, C, pooled, NP, C, NP, G, dfcW, NP, sw=sw)
+        K.colsum(dcode, out=dfcb, sw=sw)
+        grads[30], grads[31] = dfcW, dfcb
         # per_point_out.3 (no BN): dW8 = dpp^T @ H7
-        dW8 = grad_buffer(params[28]).view(W8.shape)
+        dW8, db8 = grad_buffer(params[28]).view(W8.shape), grad_buffer(params[29])
         K.wgrad(dpp, C, Ys[6], Ys[6].shape[1], C, W8.shape[1], M, dW8, W8.shape[1],
-                pro=K.PRO_ENC, pro_s=states[6].scale, pro_t=states[6].shift)
-        grads[28], grads[29] = dW8.view(params[28].shape), K.colsum(dpp, out=grad_buffer(params[29]))
+                pro=K.PRO_ENC, pro_s=states[6].scale, pro_t=states[6].shift, sw=sw)
+        K.colsum(dpp, out=db8, sw=sw)
+        grads[28], grads[29] = dW8.view(params[28].shape), db8
         dY, Wn = dpp, W8   # gradient at the output of the layer above, and that layer's weight
         for i in range(6, -1, -1):
             Y, st = Ys[i], states[i]
@@ -174,25 +179,39 @@ class PointEncoderFn(Function):
             coefs = K.bn_bwd_finalize(bws, M, N, gs[i], st.invstd, dgamma, dbeta, rw=spec.rw)
             dYi, cs = K.bn_bwd_apply(G_, Y, False, st.mean, coefs, rw=spec.rw)
             W = Ws[i]
-            dW = grad_buffer(params[4 * i]).view(W.shape)
-            if i == 0:
-                K.wgrad(dYi, N, x, 3, N, 3, M, dW, 3)
-            else:
-                Xp, stp = Ys[i - 1], states[i - 1]
-                kin = Xp.shape[1]
-                K.wgrad(dYi, N, Xp, kin, N, kin, M, dW, W.shape[1], pro=K.PRO_ENC, pro_s=stp.scale, pro_t=stp.shift)
-                if i == 5:   # semantic columns of fuse_sem
-                    S = sem.shape[1]
-                    if spec.mode == "src":
-                        D = _group_sums(dYi, cs, N, G, GR)
-                        K.wgrad(D, N, sem, S, N, S, G, dW, W.shape[1], out_off=kin)
-                    else:
-                        K.wgrad(dYi, N, sem, S, N, S, M, dW, W.shape[1], out_off=kin)
+            dW, db = grad_buffer(params[4 * i]).view(W.shape), grad_buffer(params[4 * i + 1])
+            _enc_layer_wgrad(sw, spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW, db)
             grads[4 * i] = dW.view(params[4 * i].shape)
-            grads[4 * i + 1] = K.colsum(cs, out=grad_buffer(params[4 * i + 1]))
+            grads[4 * i + 1] = db
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
+        sw.join()
         return (None, None, None) + tuple(grads)
+
+
+def _side_work(dev):
+    """The weight-gradient side stream of a chain backward (ured_hip/sidework.py); one stream
+    while SyncBN is on (its collectives split a captured graph, which needs no open fork)."""
+    return SideWork(dev, mode=0 if syncbn.active() else None)
+
+
+def _enc_layer_wgrad(sw, spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW, db):
+    """Weight and bias gradients of TargetEncoder layer i from its dY (side-stream classes)."""
+    if i == 0:
+        K.wgrad(dYi, N, x, 3, N, 3, M, dW, 3, sw=sw)
+    else:
+        Xp, stp = Ys[i - 1], states[i - 1]
+        kin = Xp.shape[1]
+        K.wgrad(dYi, N, Xp, kin, N, kin, M, dW, W.shape[1], pro=K.PRO_ENC, pro_s=stp.scale, pro_t=stp.shift, sw=sw)
+        if i == 5:   # semantic columns of fuse_sem
+            S = sem.shape[1]
+            if spec.mode == "src":
+                # G-row GEMM on the per-group sums: short work
+                sw.small(lambda: K.wgrad(_group_sums(dYi, cs, N, G, GR), N, sem, S, N, S, G, dW, W.shape[1],
+                                         out_off=kin), dYi, cs, sem)
+            else:
+                K.wgrad(dYi, N, sem, S, N, S, M, dW, W.shape[1], out_off=kin, sw=sw)
+    K.colsum(cs, out=db, sw=sw)
 
 
 def _group_sums(dY, cs, N, G, group_rows):
@@ -275,17 +294,20 @@ class ResidualNetFn(Function):
         G, Cc = code.shape
         dev = pp.device
         grads = [None] * 14
+        sw = _side_work(dev)
         dout = dout.contiguous()
         W4 = params[12].reshape(params[12].shape[0], -1)
         No = W4.shape[0]
-        dW4 = grad_buffer(params[12]).view(W4.shape)
+        dW4, db4 = grad_buffer(params[12]).view(W4.shape), grad_buffer(params[13])
         K.wgrad(dout, No, Ys[2], Ys[2].shape[1], No, W4.shape[1], M, dW4, W4.shape[1],
-                pro=K.PRO_RES, pro_s=states[2].scale, pro_t=states[2].shift)
-        grads[12], grads[13] = dW4.view(params[12].shape), K.colsum(dout, out=grad_buffer(params[13]))
+                pro=K.PRO_RES, pro_s=states[2].scale, pro_t=states[2].shift, sw=sw)
+        K.colsum(dout, out=db4, sw=sw)
+        grads[12], grads[13] = dW4.view(params[12].shape), db4
         dY, Wn = dout, W4
         W1 = params[0].reshape(params[0].shape[0], -1)
         ld1 = W1.shape[1]
         pp_off, code_off = (Cc, 0) if code_first else (0, Cp)
+        dcode = torch.zeros(G, Cc, device=dev)
         for i in range(2, -1, -1):
             Y, st = Ys[i], states[i]
             N = Y.shape[1]
@@ -298,31 +320,34 @@ class ResidualNetFn(Function):
             coefs = K.bn_bwd_finalize(bws, M, N, params[4 * i + 2], st.invstd, dgamma, dbeta, rw=rw)
             dYi, cs = K.bn_bwd_apply(G_, Y, True, st.mean, coefs, rw=rw)
             W = params[4 * i].reshape(params[4 * i].shape[0], -1)
-            dW = grad_buffer(params[4 * i]).view(W.shape)
+            dW, db = grad_buffer(params[4 * i]).view(W.shape), grad_buffer(params[4 * i + 1])
             if i == 0:
-                K.wgrad(dYi, N, pp, Cp, N, Cp, M, dW, ld1, out_off=pp_off)
-                D = None
-                if Cc > 0:
-                    if off is not None:
-                        D = K.group_colsum(dYi, N, G, off=off)
-                    else:
-                        D = _group_sums(dYi, cs, N, G, group_rows)
-                    K.wgrad(D, N, code, Cc, N, Cc, G, dW, ld1, out_off=code_off)
+                K.wgrad(dYi, N, pp, Cp, N, Cp, M, dW, ld1, out_off=pp_off, sw=sw)
+
+                def first(N=N, dYi=dYi, cs=cs, dW=dW, db=db):    # G-row work: short kernels
+                    if Cc > 0:
+                        if off is not None:
+                            D = K.group_colsum(dYi, N, G, off=off)
+                        else:
+                            D = _group_sums(dYi, cs, N, G, group_rows)
+                        K.wgrad(D, N, code, Cc, N, Cc, G, dW, ld1, out_off=code_off)
+                        # dcode = D @ W1[:, code cols]
+                        K.gemm(G, Cc, N, D, N, W1, ld1, dcode, Cc, b_kmajor=True, B_off=code_off)
+                    K.colsum(cs, out=db)
+                sw.small(first, dYi, cs, dcode, code)
             else:
                 Xp, stp = Ys[i - 1], states[i - 1]
                 K.wgrad(dYi, N, Xp, Xp.shape[1], N, Xp.shape[1], M, dW, W.shape[1],
-                        pro=K.PRO_RES, pro_s=stp.scale, pro_t=stp.shift)
+                        pro=K.PRO_RES, pro_s=stp.scale, pro_t=stp.shift, sw=sw)
+                K.colsum(cs, out=db, sw=sw)
             grads[4 * i] = dW.view(params[4 * i].shape)
-            grads[4 * i + 1] = K.colsum(cs, out=grad_buffer(params[4 * i + 1]))
+            grads[4 * i + 1] = db
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
-        # input gradients: dpp = dY1 @ W1[:, pp cols]; dcode = D @ W1[:, code cols]
-        N1 = W1.shape[0]
+        # input gradient dpp = dY1 @ W1[:, pp cols] (dcode on the side stream, above)
         dpp = torch.empty(M, Cp, device=dev)
-        K.gemm(M, Cp, N1, dY, N1, W1, ld1, dpp, Cp, b_kmajor=True, B_off=pp_off)
-        dcode = torch.zeros(G, Cc, device=dev)
-        if Cc > 0:
-            K.gemm(G, Cc, N1, D, N1, W1, ld1, dcode, Cc, b_kmajor=True, B_off=code_off)
+        K.gemm(M, Cp, W1.shape[0], dY, W1.shape[0], W1, ld1, dpp, Cp, b_kmajor=True, B_off=pp_off)
+        sw.join()
         return (None, dpp, dcode) + tuple(grads)
 
 

@@ -116,3 +116,38 @@ def test_graph_replay_across_residual_gate(dev):
     for name in a.models:
         for (k, pa), (_, pb) in zip(a.models[name].state_dict().items(), b.models[name].state_dict().items()):
             assert torch.equal(pa, pb), (name, k)
+
+
+def test_wgrad_side_stream_equals_one_stream(dev, monkeypatch):
+    """The weight-gradient side stream (ured_hip/sidework.py) changes only where the wgrad /
+    reduce / bias-sum kernels run, not what they compute: eager steps with either side-stream
+    mode and graph-replayed steps (mode 2) equal one-stream eager steps bitwise."""
+    from dataset import synthetic
+    from engine.graph import GraphedStep
+    from engine.train import batch_to_device
+    from ured_hip import sidework
+    cfg = dict(CFG, cuda_graph=True)
+    batches = [batch_to_device(synthetic.make_batch(2, 128, 24, parts=[3, 2], seed=80 + i), dev) for i in range(3)]
+    steps = {m: _make(dev, cfg) for m in (0, 1, 2)}
+    monkeypatch.setattr(sidework, "MODE", 2)
+    gs = _make(dev, cfg)
+    g = GraphedStep(gs, batches[0], warmup=2)         # 2 eager steps on batch 0, then capture
+    for _ in range(2):
+        for m, st in steps.items():
+            monkeypatch.setattr(sidework, "MODE", m)
+            st.step(batches[0])
+    for rnd in range(2):
+        for i, bt in enumerate(batches):
+            monkeypatch.setattr(sidework, "MODE", 2)
+            lg = g.step(bt)["all_loss"].clone()
+            ls = {}
+            for m, st in steps.items():
+                monkeypatch.setattr(sidework, "MODE", m)
+                ls[m] = st.step(bt)["all_loss"]
+            assert all(torch.equal(v, ls[0]) for v in ls.values()), (rnd, i, {m: v.item() for m, v in ls.items()})
+            assert torch.equal(lg, ls[0]), (rnd, i, lg.item(), ls[0].item())
+    for name in gs.models:
+        ref = list(steps[0].models[name].state_dict().items())
+        for other in (steps[1], steps[2], gs):
+            for (k, pa), (_, pb) in zip(ref, other.models[name].state_dict().items()):
+                assert torch.equal(pa, pb), (name, k)
