@@ -304,6 +304,81 @@ struct InTile {
     }
 };
 
+// BN-backward epilogue of a full 128x128 tile (every row < M, every column < N; no per-element
+// residual gradient, pooled gradients only of 128-row-aligned groups): the general loop below
+// without its per-element bounds selects, and with the Yp loads / G stores addressed as a per-lane
+// buffer offset plus a scalar row offset (no per-element 32-bit multiplies). Same operations in the
+// same order as the general loop, so the results are bitwise the same.
+template <int ACT, bool POOL, class Pre>
+__device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2][2], int m0, int n0, float (&s1)[2],
+                                           float (&s2)[2], Pre pre) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
+    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(d.Yp), (short)0,
+                                                                         (int)(((long long)(d.M - 1) * d.ldy + d.N) * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(d.C, (short)0,
+                                                                         (int)(((long long)(d.M - 1) * d.ldc + d.N) * 4), 0x00020000);
+    const unsigned ly = (unsigned)d.ldy * 4u, lc = (unsigned)d.ldc * 4u;
+    const unsigned r0 = (unsigned)(m0 + wm * 64 + 4 * (lane >> 5));       // this lane's first row
+    // rows of element (i, r): r0 + i*32 + (r&3) + 8*(r>>2) -> scalar offset (i*32 + (r&3) + 8*(r>>2)) * ld,
+    // from an opaque copy of ld so that the products are s_muls at their use, not hoisted SGPRs
+    auto roff = [&](int i, int r, unsigned ld) {
+        asm volatile("" : "+s"(ld));
+        return (unsigned)(i * 32 + (r & 3) + 8 * (r >> 2)) * ld;
+    };
+    float yh[2][2][16];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const unsigned vo = r0 * ly + (unsigned)(n0 + wn * 64 + j * 32 + (lane & 31)) * 4u;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                yh[j][i][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(yr, vo, roff(i, r, ly), 0));
+    }
+    float sc_[2], sh_[2], mu_[2], is_[2], pgr_[2];
+    int pidx_[2];
+    const int pg = POOL ? m0 / d.pool_group_rows : 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+        sc_[j] = d.bn_scale[col]; sh_[j] = d.bn_shift[col]; mu_[j] = d.bn_mean[col]; is_[j] = d.bn_invstd[col];
+        pidx_[j] = -1; pgr_[j] = 0.f;
+        if (POOL) { pidx_[j] = d.pool_idx[(size_t)pg * d.N + col]; pgr_[j] = d.pool_grad[(size_t)pg * d.N + col]; }
+    }
+    pre();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const unsigned vo = r0 * lc + (unsigned)(n0 + wn * 64 + j * 32 + (lane & 31)) * 4u;
+        const int prow = pidx_[j] - (int)r0;       // the pooled winner's row relative to this lane's first row
+        float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float a = acc[i][j][r];
+                const float dh = (POOL && prow == i * 32 + (r & 3) + 8 * (r >> 2)) ? a + pgr_[j] : a;
+                const float y = yh[j][i][r];
+                float g, xh;
+                if (ACT == URED_ACT_RES) {
+                    g = dh;
+                    xh = (fmaxf(y, 0.f) - mu_[j]) * is_[j];
+                } else if (ACT == URED_ACT_BN) {
+                    g = dh;
+                    xh = (y - mu_[j]) * is_[j];
+                } else {
+                    g = (__builtin_fmaf(y, sc_[j], sh_[j]) > 0.f) ? dh : 0.f;
+                    xh = (y - mu_[j]) * is_[j];
+                }
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, g), cr, vo, roff(i, r, lc), 0);
+                a1 += g;
+                a2 += g * xh;
+            }
+        a1 += __shfl_xor(a1, 32);
+        a2 += __shfl_xor(a2, 32);
+        s1[j] = a1; s2[j] = a2;
+    }
+}
+
 template <int EPI, bool BUFST = false, bool YL = false, class Pre = NoPre>
 __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2], int m0, int n0,
                                          float* red_f, int* red_i, Pre pre = Pre(),
@@ -498,6 +573,19 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
 
     if (EPI == URED_EPI_BNBWD) {
         float s1[2], s2[2];
+        const bool pool_al = d.pool_idx && (d.pool_group_rows % BM == 0);
+        const bool full = BUFST && !YL && m0 + BM <= d.M && n0 + BN <= d.N && !d.gadd && (!d.pool_idx || pool_al);
+        if (full) {
+            if (pool_al) {
+                if (d.bwd_res == URED_ACT_RES) bnbwd_full<URED_ACT_RES, true>(d, acc, m0, n0, s1, s2, pre);
+                else if (d.bwd_res == URED_ACT_BN) bnbwd_full<URED_ACT_BN, true>(d, acc, m0, n0, s1, s2, pre);
+                else bnbwd_full<URED_ACT_ENC, true>(d, acc, m0, n0, s1, s2, pre);
+            } else {
+                if (d.bwd_res == URED_ACT_RES) bnbwd_full<URED_ACT_RES, false>(d, acc, m0, n0, s1, s2, pre);
+                else if (d.bwd_res == URED_ACT_BN) bnbwd_full<URED_ACT_BN, false>(d, acc, m0, n0, s1, s2, pre);
+                else bnbwd_full<URED_ACT_ENC, false>(d, acc, m0, n0, s1, s2, pre);
+            }
+        } else {
         // Yp one column half (32 values) at a time: the j = 0 half and the per-column
         // parameters are issued before pre() (the persistent kernel's next-tile DMA), the j = 1
         // half after the j = 0 half is processed (registers: acc 64 + one half 32)
@@ -618,6 +706,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             a2 += __shfl_xor(a2, 32);
             s1[j] = a1; s2[j] = a2;
         }
+        }   // general loop
         if (lane < 32) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -1096,8 +1185,21 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             }
         };
         if (YPL && !has_k) { yp_dma(0, stage); yp_dma(1, stage ^ 1); }
+#ifdef URED_EXP_NOEPI   // timing experiment only (wrong results): the tile's sum, one store per lane
+        {
+            float sacc = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) sacc += acc[i][j][r];
+            if (sacc == 1234.5f) d.C[t] = sacc;
+        }
+#else
         epilogue<EPI, true, YPL>(d, acc, m0, n0, red_f, red_i, pre, smem + stage * 2 * TILE,
                                  smem + (stage ^ 1) * 2 * TILE);
+#endif
         if (!GEMM_PERSIST || nv >= ntiles) break;
         v = nv; m0 = nm0; n0 = nn0;
         after_epi = true;
