@@ -33,6 +33,9 @@ constexpr int NN_THREADS = 256;
 constexpr int NN_TILE = 1024;   // refs per LDS tile (12 KiB SoA)
 constexpr int NN_CHUNK = 16;    // refs per min-tracking chunk
 constexpr float NN_PAD = 1.0e30f;  // padding coordinate: distance overflows to +inf
+#ifndef URED_NN_TILE_ALL
+#define URED_NN_TILE_ALL 1
+#endif
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -65,14 +68,19 @@ __device__ __forceinline__ void resolve_pair(const NNFwdArgs& A, int dir, int s,
     else          { Q = A.b; R = A.a; q_off = bo; q_len = bl; r_off = ao; r_len = al; dist = A.dist_b; idx = A.idx_b; }
 }
 
-template <int QPT, int RS>
+// TILE: refs per LDS fill. The whole-set variant (TILE = NN_TILE_ALL, used when every segment's
+// refs fit) fills LDS once and takes the argmin rescan of the winning chunk from LDS too, so a
+// small launch pays one fill and no dependent global reads at the end.
+constexpr int NN_TILE_ALL = 4096;   // 48 KiB SoA
+template <int QPT, int RS, int TILE = NN_TILE>
 __global__ __launch_bounds__(NN_THREADS) void nn_fwd_kernel(NNFwdArgs args) {
     constexpr int G = NN_THREADS / RS;      // threads per ref-split group
     constexpr int QB = G * QPT;             // queries per block
-    constexpr int SUB = NN_TILE / RS;       // refs per group per tile
-    __shared__ __attribute__((aligned(16))) float sx[NN_TILE];
-    __shared__ __attribute__((aligned(16))) float sy[NN_TILE];
-    __shared__ __attribute__((aligned(16))) float sz[NN_TILE];
+    constexpr int SUB = TILE / RS;          // refs per group per tile
+    constexpr bool ALL = TILE == NN_TILE_ALL;
+    __shared__ __attribute__((aligned(16))) float sx[TILE];
+    __shared__ __attribute__((aligned(16))) float sy[TILE];
+    __shared__ __attribute__((aligned(16))) float sz[TILE];
     __shared__ float mbest[RS > 1 ? RS * QB : 1];
     __shared__ int mchunk[RS > 1 ? RS * QB : 1];
 
@@ -101,10 +109,13 @@ __global__ __launch_bounds__(NN_THREADS) void nn_fwd_kernel(NNFwdArgs args) {
         bchunk[i] = 0;
     }
 
-    for (int t0 = 0; t0 < r_len; t0 += NN_TILE) {
-        const int tn = min(NN_TILE, r_len - t0);
+    for (int t0 = 0; t0 < r_len; t0 += TILE) {
+        const int tn = min(TILE, r_len - t0);
+        // refs per group: SUB, or (whole-set tile) the fill split evenly over the RS groups in
+        // whole chunks (RS * sub <= TILE, since TILE is a multiple of RS * NN_CHUNK)
+        const int sub = ALL ? ((tn + RS - 1) / RS + NN_CHUNK - 1) / NN_CHUNK * NN_CHUNK : SUB;
         __syncthreads();
-        for (int i = t; i < NN_TILE; i += NN_THREADS) {
+        for (int i = t; i < (ALL ? RS * sub : TILE); i += NN_THREADS) {
             float x = NN_PAD, y = NN_PAD, z = NN_PAD;
             if (i < tn) {
                 const float* p = R + 3 * (size_t)(r_off + t0 + i);
@@ -114,8 +125,8 @@ __global__ __launch_bounds__(NN_THREADS) void nn_fwd_kernel(NNFwdArgs args) {
         }
         __syncthreads();
         // this group's sub-range of the tile, in chunks of NN_CHUNK
-        const int base = g * SUB;
-        const int sub_n = min(SUB, max(0, tn - base));
+        const int base = g * sub;
+        const int sub_n = min(sub, max(0, tn - base));
         const int nch = (sub_n + NN_CHUNK - 1) / NN_CHUNK;
         const int chunk0 = (t0 + base) / NN_CHUNK;
         for (int c = 0; c < nch; ++c) {
@@ -173,8 +184,13 @@ __global__ __launch_bounds__(NN_THREADS) void nn_fwd_kernel(NNFwdArgs args) {
         const int kn = min(NN_CHUNK, r_len - k0);
         int bi = k0;
         for (int k = 0; k < kn; ++k) {
-            const float* p = R + 3 * (size_t)(r_off + k0 + k);
-            if (sqd(qx[i], qy[i], qz[i], p[0], p[1], p[2]) == best[i]) { bi = k0 + k; break; }
+            float rx, ry, rz;
+            if constexpr (ALL) { rx = sx[k0 + k]; ry = sy[k0 + k]; rz = sz[k0 + k]; }
+            else {
+                const float* p = R + 3 * (size_t)(r_off + k0 + k);
+                rx = p[0]; ry = p[1]; rz = p[2];
+            }
+            if (sqd(qx[i], qy[i], qz[i], rx, ry, rz) == best[i]) { bi = k0 + k; break; }
         }
         dist[q_off + qi] = best[i];
         idx[q_off + qi] = bi;
@@ -263,10 +279,13 @@ __global__ __launch_bounds__(NN_THREADS) void nn_bwd_kernel(NNBwdArgs args) {
 }
 
 template <int QPT, int RS>
-void launch_fwd(const NNFwdArgs& a, int max_q, int nseg, int ndirs, hipStream_t st) {
+void launch_fwd(const NNFwdArgs& a, int max_q, int max_r, int nseg, int ndirs, hipStream_t st) {
     constexpr int QB = (NN_THREADS / RS) * QPT;
     dim3 grid((max_q + QB - 1) / QB, nseg, ndirs);
-    hipLaunchKernelGGL((nn_fwd_kernel<QPT, RS>), grid, dim3(NN_THREADS), 0, st, a);
+    if (URED_NN_TILE_ALL && max_r <= NN_TILE_ALL)
+        hipLaunchKernelGGL((nn_fwd_kernel<QPT, RS, NN_TILE_ALL>), grid, dim3(NN_THREADS), 0, st, a);
+    else
+        hipLaunchKernelGGL((nn_fwd_kernel<QPT, RS>), grid, dim3(NN_THREADS), 0, st, a);
 }
 
 // Pick queries-per-thread / ref-split so that the launch has enough waves for 256 CUs.
@@ -279,9 +298,22 @@ int fwd_dispatch(const NNFwdArgs& a, int nseg, int max_a, int max_b, hipStream_t
     if (max_q <= 0 || nseg <= 0) return 0;
     // waves launched with QPT=2, RS=1: 4 waves per 512 queries
     const long long waves1 = (total_q + 511) / 512 * 4;
-    if (waves1 >= 4096 || max_r < 4 * NN_TILE / 4) launch_fwd<2, 1>(a, max_q, nseg, ndirs, st);
-    else if (waves1 >= 2048) launch_fwd<2, 2>(a, max_q, nseg, ndirs, st);
-    else launch_fwd<2, 4>(a, max_q, nseg, ndirs, st);
+#ifdef URED_NN_CFG_ENV   // experiment: force (QPT, RS) from URED_NN_CFG="qpt,rs"
+    static const int cfg = [] { const char* e = getenv("URED_NN_CFG"); return e ? (e[0] - '0') * 10 + (e[1] - '0') : 0; }();
+    switch (cfg) {
+        case 24: launch_fwd<2, 4>(a, max_q, max_r, nseg, ndirs, st); return 0;
+        case 28: launch_fwd<2, 8>(a, max_q, max_r, nseg, ndirs, st); return 0;
+        case 44: launch_fwd<4, 4>(a, max_q, max_r, nseg, ndirs, st); return 0;
+        case 48: launch_fwd<4, 8>(a, max_q, max_r, nseg, ndirs, st); return 0;
+        case 42: launch_fwd<4, 2>(a, max_q, max_r, nseg, ndirs, st); return 0;
+        case 14: launch_fwd<1, 4>(a, max_q, max_r, nseg, ndirs, st); return 0;
+        case 18: launch_fwd<1, 8>(a, max_q, max_r, nseg, ndirs, st); return 0;
+        default: break;
+    }
+#endif
+    if (waves1 >= 4096 || max_r < 4 * NN_TILE / 4) launch_fwd<2, 1>(a, max_q, max_r, nseg, ndirs, st);
+    else if (waves1 >= 2048) launch_fwd<2, 2>(a, max_q, max_r, nseg, ndirs, st);
+    else launch_fwd<2, 4>(a, max_q, max_r, nseg, ndirs, st);
     return 0;
 }
 

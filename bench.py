@@ -247,7 +247,11 @@ def cpu_baseline(args):
 def chamfer_rate(dev, B=16, n=2048, m=2048, iters=20):
     """NN forward (both directions) on one dense [B,n,3] x [B,m,3] call: Gpair-dist/s and the
     two SURVEY §8(d) roofline fractions (8 FLOP/pair vs 157.3 TFLOP/s FP32 VALU — the binding
-    roof; 12 B/point read vs 8 TB/s HBM — the north star's, unattainable by construction)."""
+    roof; 12 B/point read vs 8 TB/s HBM — the north star's, unattainable by construction).
+    `ms` is the device time per call: `iters` calls captured in one HIP graph and replayed, so the
+    Python / autograd / allocation cost of issuing each call (tens of µs on the host, the same
+    order as the kernel at this size) is not in it; `ms_eager` times the same calls issued one by
+    one from Python."""
     from ured_hip import nn as unn
     g = torch.Generator().manual_seed(0)
     p1 = torch.rand(B, n, 3, generator=g).to(dev)
@@ -261,9 +265,29 @@ def chamfer_rate(dev, B=16, n=2048, m=2048, iters=20):
         unn.nn_dense(p1, p2)
     e1.record()
     torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / iters * 1e-3
+    t_eager = e0.elapsed_time(e1) / iters * 1e-3
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        unn.nn_dense(p1, p2)                 # warm the side stream's allocator pool
+        with torch.cuda.graph(graph):
+            for _ in range(iters):
+                unn.nn_dense(p1, p2)
+    torch.cuda.current_stream().wait_stream(side)
+    graph.replay()
+    torch.cuda.synchronize()
+    reps = 5
+    e0.record()
+    for _ in range(reps):
+        graph.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / (reps * iters) * 1e-3
     pairs = B * n * m
     return {"shape": f"{B}x{n}x{m}", "ms": round(t * 1e3, 4), "gpair_dist_s": round(pairs / t / 1e9, 1),
+            "ms_eager": round(t_eager * 1e3, 4), "gpair_dist_s_eager": round(pairs / t_eager / 1e9, 1),
+            "timing": f"{iters} calls in one HIP graph, replayed {reps}x",
             "path": "fused" if pairs >= unn.FUSED_MIN_PAIRS else "two-pass",
             "valu_frac": round(8 * pairs / t / 157.3e12, 4),
             "hbm_read_frac": round(12 * B * (n + m) / t / 8e12, 6)}
