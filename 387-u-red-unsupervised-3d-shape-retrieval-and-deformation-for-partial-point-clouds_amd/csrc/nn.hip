@@ -298,22 +298,16 @@ int fwd_dispatch(const NNFwdArgs& a, int nseg, int max_a, int max_b, hipStream_t
     if (max_q <= 0 || nseg <= 0) return 0;
     // waves launched with QPT=2, RS=1: 4 waves per 512 queries
     const long long waves1 = (total_q + 511) / 512 * 4;
-#ifdef URED_NN_CFG_ENV   // experiment: force (QPT, RS) from URED_NN_CFG="qpt,rs"
-    static const int cfg = [] { const char* e = getenv("URED_NN_CFG"); return e ? (e[0] - '0') * 10 + (e[1] - '0') : 0; }();
-    switch (cfg) {
-        case 24: launch_fwd<2, 4>(a, max_q, max_r, nseg, ndirs, st); return 0;
-        case 28: launch_fwd<2, 8>(a, max_q, max_r, nseg, ndirs, st); return 0;
-        case 44: launch_fwd<4, 4>(a, max_q, max_r, nseg, ndirs, st); return 0;
-        case 48: launch_fwd<4, 8>(a, max_q, max_r, nseg, ndirs, st); return 0;
-        case 42: launch_fwd<4, 2>(a, max_q, max_r, nseg, ndirs, st); return 0;
-        case 14: launch_fwd<1, 4>(a, max_q, max_r, nseg, ndirs, st); return 0;
-        case 18: launch_fwd<1, 8>(a, max_q, max_r, nseg, ndirs, st); return 0;
-        default: break;
-    }
-#endif
-    if (waves1 >= 4096 || max_r < 4 * NN_TILE / 4) launch_fwd<2, 1>(a, max_q, max_r, nseg, ndirs, st);
+    // about 2048 waves (two per SIMD) or as close as the splits allow; with the whole-set tile
+    // a small ref set splits evenly too. Measured (graph-replayed, tools/chamfer_rates.py):
+    // 16x2048x2048 <2,4> 26.1 us (<1,4> 26.9, <1,8> 30.8); 32x2000x1000 <2,4> 32.7 (<1,8> 33.4);
+    // 2x512x512 <1,8> 5.4 (<2,4> 8.3, <2,1> 15.6)
+    const bool all = URED_NN_TILE_ALL && max_r <= NN_TILE_ALL;
+    if (waves1 >= 4096 || (!all && max_r < NN_TILE)) launch_fwd<2, 1>(a, max_q, max_r, nseg, ndirs, st);
     else if (waves1 >= 2048) launch_fwd<2, 2>(a, max_q, max_r, nseg, ndirs, st);
-    else launch_fwd<2, 4>(a, max_q, max_r, nseg, ndirs, st);
+    else if (waves1 >= 512 || !all) launch_fwd<2, 4>(a, max_q, max_r, nseg, ndirs, st);
+    else if (waves1 >= 256) launch_fwd<1, 4>(a, max_q, max_r, nseg, ndirs, st);
+    else launch_fwd<1, 8>(a, max_q, max_r, nseg, ndirs, st);
     return 0;
 }
 

@@ -17,12 +17,24 @@ from . import _lib
 FUSED = True
 # Below ~1e8 pairs a launch is latency-bound and the two-pass kernel (one launch, no
 # finalize) is faster on MI355X (16x2048x2048: 30 vs 39 us); from there up the fused one
-# (64x4096x4096: 1.27x, ragged 16x16384x2048: 4.3x, 4096x1024x1024: 1.15x).
+# (64x4096x4096: 1.27x, ragged 16x16384x2048: 4.3x, 4096x1024x1024: 1.15x). When every
+# segment's point sets fit the two-pass kernel's whole-set LDS tile (<= 4096 points) it stays
+# ahead up to ~5e8 pairs (graph-replayed, tools/chamfer_rates.py: 8x4096x4096 42 vs 63 us,
+# 16x4096x4096 75 vs 89 us; 64x4096x4096 fused 218 vs 284 us).
 FUSED_MIN_PAIRS = 96 << 20
+FUSED_MIN_PAIRS_SMALL_SETS = 512 << 20
+TWO_PASS_ALL_TILE = 4096         # NN_TILE_ALL (csrc/nn.hip)
+
+
+def use_fused(nseg, max_a, max_b):
+    """Whether a launch of nseg segments of at most max_a x max_b points takes the fused path."""
+    pairs = nseg * max_a * max_b
+    small_sets = max(max_a, max_b) <= TWO_PASS_ALL_TILE
+    return FUSED and pairs >= (FUSED_MIN_PAIRS_SMALL_SETS if small_sets else FUSED_MIN_PAIRS)
 
 
 def _workspace(nseg, max_a, max_b, a_total, b_total, dirs, dev):
-    if not FUSED or nseg * max_a * max_b < FUSED_MIN_PAIRS:
+    if not use_fused(nseg, max_a, max_b):
         return None, 0
     nbytes = _lib.query("ured_nn_fwd_workspace", nseg, max_a, max_b, a_total, b_total, dirs)
     if nbytes == 0:

@@ -288,7 +288,7 @@ def chamfer_rate(dev, B=16, n=2048, m=2048, iters=20):
     return {"shape": f"{B}x{n}x{m}", "ms": round(t * 1e3, 4), "gpair_dist_s": round(pairs / t / 1e9, 1),
             "ms_eager": round(t_eager * 1e3, 4), "gpair_dist_s_eager": round(pairs / t_eager / 1e9, 1),
             "timing": f"{iters} calls in one HIP graph, replayed {reps}x",
-            "path": "fused" if pairs >= unn.FUSED_MIN_PAIRS else "two-pass",
+            "path": "fused" if unn.use_fused(B, n, m) else "two-pass",
             "valu_frac": round(8 * pairs / t / 157.3e12, 4),
             "hbm_read_frac": round(12 * B * (n + m) / t / 8e12, 6)}
 

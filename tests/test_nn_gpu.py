@@ -21,9 +21,10 @@ def _rand(shape, seed):
 
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("b,n,m", [(4, 100, 200), (3, 257, 129), (2, 1, 5), (1, 2048, 2048), (2, 1023, 1025),
-                                   (5, 3000, 17), (1, 17, 4100)])
+                                   (5, 3000, 17), (1, 17, 4100), (2, 512, 512), (1, 4096, 3000), (3, 4096, 33)])
 def test_dense_fwd_bitexact(unn, dev, b, n, m, fused, monkeypatch):
     monkeypatch.setattr(unn, "FUSED_MIN_PAIRS", 0 if fused else 1 << 62)
+    monkeypatch.setattr(unn, "FUSED_MIN_PAIRS_SMALL_SETS", 0 if fused else 1 << 62)
     p1, p2 = _rand((b, n, 3), n), _rand((b, m, 3), m + 7)
     d1, d2, i1, i2 = unn.nn_dense(torch.from_numpy(p1).to(dev), torch.from_numpy(p2).to(dev))
     r = nn_ref.nn_fwd(p1, p2)
@@ -171,6 +172,7 @@ def test_errors_raise(unn, dev):
 def fused_always(unn, monkeypatch):
     """Fused path at every size (the wrapper otherwise keeps small launches two-pass)."""
     monkeypatch.setattr(unn, "FUSED_MIN_PAIRS", 0)
+    monkeypatch.setattr(unn, "FUSED_MIN_PAIRS_SMALL_SETS", 0)
 
 
 @pytest.fixture
