@@ -103,7 +103,8 @@ class GraphedStep:
 
     def key(self, batch, epoch=0):
         uq = batch.get("src_unique")
-        return (None if uq is None else uq.U, self.gate(epoch))
+        pb = batch.get("part_bounds")          # sizes the loss head's NN launches (ured_hip/ops.py)
+        return (None if uq is None else uq.U, self.gate(epoch), None if pb is None else pb.key())
 
     def _flat(self):
         """FlatAdam: the HIP layers write the gradients into its persistent flat buffer."""

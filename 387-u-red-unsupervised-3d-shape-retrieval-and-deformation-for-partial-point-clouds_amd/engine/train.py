@@ -51,7 +51,7 @@ from network.simple_encoder import TargetEncoder as simple_encoder  # noqa: E402
 from train_utils.load_sources import load_sources  # noqa: E402
 from train_utils.optimizer_dm import define_optimizer_dm_re_recon  # noqa: E402
 from ured_hip.kernels import RowWeights  # noqa: E402
-from ured_hip.ops import UniqueRows, build_parts, part_aabb, part_rows, upload  # noqa: E402
+from ured_hip.ops import PartBounds, UniqueRows, build_parts, part_aabb, part_rows, upload  # noqa: E402
 
 MODULE_NAMES = ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "re_residual_net_full",
                 "src_encoder_all", "recon_decoder_src", "embedding_layer")
@@ -281,7 +281,8 @@ class TrainStep:
             contrast_ext = compute_contrast_loss_loss(target_part_f, codes, contrast_labels,
                                                       cfg.get("differentiable_gather", False))
         hi = HeadInputs(x, parts, self.np_per_part, src_labels, pts_u, inv, cfg,
-                        gate=cfg.get("use_residuals_reg", 0.0) > 0.0 and epoch > cfg["init_p_m_loss"])
+                        gate=cfg.get("use_residuals_reg", 0.0) > 0.0 and epoch > cfg["init_p_m_loss"],
+                        bounds=batch.get("part_bounds"))
         loss, T, _ = loss_head(hi, out, re_res, recon_full_p, rec_u, target_part_f, codes, param, contrast_ext)
         T["all_loss"] = loss
         T["_out"] = out
@@ -429,6 +430,7 @@ def batch_to_device(b, device, num_sources=None, bucket=None):
     TrainStep unless cfg["unique_sources"] is False); `bucket` pads their count for HIP-graph
     replay (engine/graph.py keeps one graph per padded count)."""
     out = {k: upload(b[k], device) for k in ("x", "labels", "tgt_sem", "src_labels")}
+    out["part_bounds"] = PartBounds(b["labels"])
     if num_sources is not None:
         out["src_unique"] = UniqueRows(b["src_labels"], num_sources, device, bucket=bucket)
     return out

@@ -21,6 +21,7 @@ Terms vector layout (slots): 0 cd_full, 1 cd_part, 2 ref_cd_full, 3 ref_cd_part,
 """
 import ctypes
 import math
+import os
 
 import torch
 from torch.autograd import Function
@@ -38,6 +39,7 @@ class PointLossDesc(ctypes.Structure):
 
 
 ASSEMBLE_MAX = 16
+USE_PART_BOUNDS = os.environ.get("URED_PART_BOUNDS", "1") != "0"   # A/B knob: 0 = slot bounds
 _lib.register({
     "ured_cd_pair_prep": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "ured_cd_pair_reduce": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P],
@@ -101,9 +103,19 @@ class HeadInputs:
     for the weighted source reconstruction; cfg: the loss weights (use_* keys); gate: whether the
     residual loss is on this epoch (engine/train.py:308)."""
 
-    def __init__(self, x, parts, np_per_part, src_labels, ptsu, inv, cfg, gate):
+    def __init__(self, x, parts, np_per_part, src_labels, ptsu, inv, cfg, gate, bounds=None):
         self.x, self.parts, self.np, self.src_labels = x, parts, int(np_per_part), src_labels
         self.ptsu, self.inv, self.cfg, self.gate = ptsu, inv, cfg, bool(gate)
+        self.bounds = bounds
+
+    def nn_bounds(self, S, N):
+        """(full-family a bound, part-family b bound) of the chamfer NN launches: the slot bounds
+        (S deformed points, N target points) or, with the batch's host-side PartBounds, the most
+        parts x points per part and the largest part (every segment lies within them)."""
+        b = self.bounds
+        if b is None or not USE_PART_BOUNDS:
+            return S, N
+        return min(S, b.k * self.np), min(N, b.count)
 
     def weights(self):
         """(slot order list for the forward sum, per-slot weights for the backward)."""
@@ -148,8 +160,9 @@ class LossHeadFn(Function):
         _lib.call("ured_cd_pair_prep", _p(out), _p(x), _p(parts.x_sorted.contiguous()), _p(k), _p(counts), _p(off),
                   B, S, N, P, NP, _p(A), _p(X2), _p(XS2), _p(segf), _p(segp), st)
         Af, X2f, XS2f = A.view(-1, 3), X2.view(-1, 3), XS2.view(-1, 3)
-        daf, iaf, dbf, ibf = _nn_seg(Af, X2f, segf, S, N)
-        dap, iap, dbp, ibp = _nn_seg(Af, XS2f, segp, NP, N)
+        Sb, Nb = hi.nn_bounds(S, N)
+        daf, iaf, dbf, ibf = _nn_seg(Af, X2f, segf, Sb, N)
+        dap, iap, dbp, ibp = _nn_seg(Af, XS2f, segp, NP, Nb)
         ws = torch.empty(3 * 2 * B * (P + 1), device=dev)
         _lib.call("ured_cd_pair_reduce", _p(daf), _p(dbf), _p(dap), _p(dbp), _p(k), _p(counts), _p(off),
                   B, S, N, P, NP, _p(ws), _counter(dev, 0), _p(T), st)
@@ -246,9 +259,10 @@ class LossHeadFn(Function):
         _lib.call("ured_cd_pair_grad", _p(gv), _p(k), _p(counts), _p(parts.gid.contiguous()), B, S, N, P, NP,
                   _p(gaf), _p(gbf), _p(gap), _p(gbp), _p(ga), st)
         Af, X2f, XS2f = A.view(-1, 3), X2.view(-1, 3), XS2.view(-1, 3)
-        _lib.call("ured_nn_seg_bwd", _p(Af), _p(X2f), _p(segf), segf.shape[0], S, N, _p(gaf), _p(gbf),
+        Sb, Nb = hi.nn_bounds(S, N)
+        _lib.call("ured_nn_seg_bwd", _p(Af), _p(X2f), _p(segf), segf.shape[0], Sb, N, _p(gaf), _p(gbf),
                   _p(iaf), _p(ibf), _p(ga), None, st)
-        _lib.call("ured_nn_seg_bwd", _p(Af), _p(XS2f), _p(segp), segp.shape[0], NP, N, _p(gap), _p(gbp),
+        _lib.call("ured_nn_seg_bwd", _p(Af), _p(XS2f), _p(segp), segp.shape[0], NP, Nb, _p(gap), _p(gbp),
                   _p(iap), _p(ibp), _p(ga), None, st)
         g_out = torch.empty(B, S, 3, device=dev)
         _lib.call("ured_cd_pair_fold", _p(ga), B, S, _p(g_out), st)

@@ -241,6 +241,37 @@ def upload(a, device):
     return t.pin_memory().to(device, non_blocking=True)
 
 
+class PartBounds:
+    """Host-side bounds of a target batch's part structure, from the host labels (no device sync):
+    k = the most parts of any target (rounded up to a multiple of 4) and count = the most points of
+    any one part (rounded up to a multiple of 256). The loss head sizes its chamfer NN launches by
+    them instead of by the slot bounds (P x 1024 deformed points, N target points per part): with
+    the step's 4 parts per target the full family is 4096 x 2048 per target instead of 16384 x
+    2048, small enough for the two-pass kernel's whole-set tile. Part of the HIP-graph key
+    (engine/graph.py); rounding keeps the number of distinct keys small."""
+
+    def __init__(self, labels_host):
+        import numpy as np
+        lab = np.asarray(labels_host)
+        lab = lab.reshape(lab.shape[0], -1)
+        k = cnt = 0
+        for row in lab:
+            _, c = np.unique(row, return_counts=True)
+            k, cnt = max(k, int(c.shape[0])), max(cnt, int(c.max()) if c.size else 0)
+        self.k = -(-k // 4) * 4
+        self.count = -(-cnt // 256) * 256
+
+    def key(self):
+        return (self.k, self.count)
+
+    def clone(self):
+        return self
+
+    def copy_(self, other, non_blocking=False):
+        assert other.key() == self.key(), "PartBounds.copy_: different bounds (part of the graph key)"
+        return self
+
+
 class UniqueRows:
     """Distinct entries of a batch of source-part slots (engine/train.py:196-211: every slot
     whose label is -1 — and any repeated label — encodes the same source part).

@@ -51,7 +51,7 @@ def test_graph_replay_unique_sources_equals_eager(dev):
     parts = [[3, 2], [5, 4], [3, 2], [5, 4], [2, 2]]
     batches = [batch_to_device(synthetic.make_batch(2, 128, 24, parts=p, seed=70 + i), dev, 24, bucket=4)
                for i, p in enumerate(parts)]
-    keys = {b["src_unique"].U for b in batches}
+    keys = {(b["src_unique"].U, b["part_bounds"].key()) for b in batches}   # GraphedStep.key's batch part
     assert len(keys) >= 2
     a, b = _make(dev, cfg), _make(dev, cfg)
     g = GraphedStep(a)

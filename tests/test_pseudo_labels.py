@@ -130,3 +130,20 @@ def test_table_matches_reference_golden(device, request):
                            cl_k=int(g["cl_k"]), device=device)
     got = tab.labels(torch.from_numpy(g["part_rows"]).to(device)).cpu().numpy()
     np.testing.assert_array_equal(got, g["source_labels"])
+
+
+def test_part_bounds_cover_every_part():
+    """PartBounds (the loss head's NN launch bounds) are >= the parts per target and the points
+    per part of every target, rounded up (4 parts, 256 points), from the host labels alone."""
+    from ured_hip.ops import PartBounds
+    rng = np.random.default_rng(5)
+    for trial in range(20):
+        B, N = int(rng.integers(1, 5)), int(rng.integers(1, 3000))
+        k = rng.integers(1, 17, size=B)
+        lab = np.stack([rng.integers(0, kk, size=N) for kk in k])
+        pb = PartBounds(lab)
+        for row in lab:
+            _, c = np.unique(row, return_counts=True)
+            assert c.shape[0] <= pb.k and c.max() <= pb.count
+        assert pb.k % 4 == 0 and pb.count % 256 == 0
+        assert pb.k - max(np.unique(r).shape[0] for r in lab) < 4
