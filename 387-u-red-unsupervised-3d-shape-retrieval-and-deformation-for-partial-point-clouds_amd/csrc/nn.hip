@@ -302,9 +302,12 @@ int fwd_dispatch(const NNFwdArgs& a, int nseg, int max_a, int max_b, hipStream_t
     // a small ref set splits evenly too. Measured (graph-replayed, tools/chamfer_rates.py):
     // 16x2048x2048 <2,4> 26.1 us (<1,4> 26.9, <1,8> 30.8); 32x2000x1000 <2,4> 32.7 (<1,8> 33.4);
     // 2x512x512 <1,8> 5.4 (<2,4> 8.3, <2,1> 15.6)
+    // With the whole-set tile the split is at least 4 ref groups: a ragged launch (the loss head's
+    // part family: 512 segments, a quarter of them non-empty) is sized by its bounds, so waves1
+    // overstates its work; 4 groups cost one small LDS combine where the bound is tight.
     const bool all = URED_NN_TILE_ALL && max_r <= NN_TILE_ALL;
-    if (waves1 >= 4096 || (!all && max_r < NN_TILE)) launch_fwd<2, 1>(a, max_q, max_r, nseg, ndirs, st);
-    else if (waves1 >= 2048) launch_fwd<2, 2>(a, max_q, max_r, nseg, ndirs, st);
+    if (!all && (waves1 >= 4096 || max_r < NN_TILE)) launch_fwd<2, 1>(a, max_q, max_r, nseg, ndirs, st);
+    else if (!all && waves1 >= 2048) launch_fwd<2, 2>(a, max_q, max_r, nseg, ndirs, st);
     else if (waves1 >= 512 || !all) launch_fwd<2, 4>(a, max_q, max_r, nseg, ndirs, st);
     else if (waves1 >= 256) launch_fwd<1, 4>(a, max_q, max_r, nseg, ndirs, st);
     else launch_fwd<1, 8>(a, max_q, max_r, nseg, ndirs, st);
