@@ -13,16 +13,19 @@ ResidualNetFn  : re_residual_net.forward (network/deformation_net.py:96-107) wit
 Both run forward and backward entirely on HIP kernels; only the tiny
 per-call index bookkeeping is Python.
 """
+import os
+
 import torch
 from torch.autograd import Function
 
 from . import _lib
 from . import kernels as K
-from . import syncbn
+from . import node, syncbn
 from .optim import grad_buffer
 from .sidework import SideWork
 
 BN_EPS = 1e-5
+_BIAS_BATCH = os.environ.get("URED_BIAS_BATCH", "1") != "0"
 
 
 class EncoderSpec:
@@ -146,6 +149,7 @@ class PointEncoderFn(Function):
         C = W8.shape[0]
         grads = [None] * 32
         sw = _side_work(dev)
+        bias = _BiasSums()
         dcode = torch.zeros(G, C, device=dev) if dcode is None else dcode.contiguous()
         dpp = torch.zeros(M, C, device=dev) if dpp is None else dpp.contiguous()
         # fc: code = pooled @ fcW^T + fcb
@@ -180,13 +184,37 @@ class PointEncoderFn(Function):
             dYi, cs = K.bn_bwd_apply(G_, Y, False, st.mean, coefs, rw=spec.rw)
             W = Ws[i]
             dW, db = grad_buffer(params[4 * i]).view(W.shape), grad_buffer(params[4 * i + 1])
-            _enc_layer_wgrad(sw, spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW, db)
+            _enc_layer_wgrad(sw, spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW)
+            bias.add(cs, db)
             grads[4 * i] = dW.view(params[4 * i].shape)
             grads[4 * i + 1] = db
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
+        bias.flush()
         sw.join()
         return (None, None, None) + tuple(grads)
+
+
+class _BiasSums:
+    """Conv-bias gradients of a chain backward: the column sums of each BN layer's per-128-row
+    partials of dY (cs [M/128, N], from the BN-backward apply), collected and issued at the end of
+    the backward as column-sum jobs of batched node-GEMM launches (csrc/node.hip, up to 6 per
+    launch) instead of one launch per layer. Nothing reads them before the optimizer."""
+
+    def __init__(self):
+        self.jobs = []
+
+    def add(self, cs, out):
+        if not _BIAS_BATCH:                  # A/B knob URED_BIAS_BATCH=0: one column-sum launch per layer
+            K.colsum(cs, out=out)
+            return out
+        self.jobs.append((cs, out))
+        return out
+
+    def flush(self):
+        if self.jobs:
+            node.launch(*[node.colsum_desc(cs, out) for cs, out in self.jobs])
+        self.jobs = []
 
 
 def _side_work(dev):
@@ -195,8 +223,8 @@ def _side_work(dev):
     return SideWork(dev, mode=0 if syncbn.active() else None)
 
 
-def _enc_layer_wgrad(sw, spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW, db):
-    """Weight and bias gradients of TargetEncoder layer i from its dY (side-stream classes)."""
+def _enc_layer_wgrad(sw, spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW):
+    """Weight gradient of TargetEncoder layer i from its dY (side-stream classes)."""
     if i == 0:
         K.wgrad(dYi, N, x, 3, N, 3, M, dW, 3, sw=sw)
     else:
@@ -211,7 +239,6 @@ def _enc_layer_wgrad(sw, spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, d
                                          out_off=kin), dYi, cs, sem)
             else:
                 K.wgrad(dYi, N, sem, S, N, S, M, dW, W.shape[1], out_off=kin, sw=sw)
-    K.colsum(cs, out=db, sw=sw)
 
 
 def _group_sums(dY, cs, N, G, group_rows):
@@ -295,6 +322,7 @@ class ResidualNetFn(Function):
         dev = pp.device
         grads = [None] * 14
         sw = _side_work(dev)
+        bias = _BiasSums()
         dout = dout.contiguous()
         W4 = params[12].reshape(params[12].shape[0], -1)
         No = W4.shape[0]
@@ -333,17 +361,17 @@ class ResidualNetFn(Function):
                         K.wgrad(D, N, code, Cc, N, Cc, G, dW, ld1, out_off=code_off)
                         # dcode = D @ W1[:, code cols]
                         K.gemm(G, Cc, N, D, N, W1, ld1, dcode, Cc, b_kmajor=True, B_off=code_off)
-                    K.colsum(cs, out=db)
                 sw.small(first, dYi, cs, dcode, code)
             else:
                 Xp, stp = Ys[i - 1], states[i - 1]
                 K.wgrad(dYi, N, Xp, Xp.shape[1], N, Xp.shape[1], M, dW, W.shape[1],
                         pro=K.PRO_RES, pro_s=stp.scale, pro_t=stp.shift, sw=sw)
-                K.colsum(cs, out=db, sw=sw)
+            bias.add(cs, db)
             grads[4 * i] = dW.view(params[4 * i].shape)
             grads[4 * i + 1] = db
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
+        bias.flush()
         # input gradient dpp = dY1 @ W1[:, pp cols] (dcode on the side stream, above)
         dpp = torch.empty(M, Cp, device=dev)
         K.gemm(M, Cp, W1.shape[0], dY, W1.shape[0], W1, ld1, dpp, Cp, b_kmajor=True, B_off=pp_off)
@@ -441,6 +469,7 @@ class PointChainFn(Function):
         use_pool = spec.pool and dpooled is not None and dpooled.numel() > 0
         use_act = spec.want_act and dact is not None and dact.numel() > 0
         dY, Wn = None, None
+        bias = _BiasSums()
         for i in range(L - 1, -1, -1):
             Y, st = Ys[i], states[i]
             N = Y.shape[1]
@@ -474,9 +503,10 @@ class PointChainFn(Function):
                 kin = Xp.shape[1]
                 K.wgrad(dYi, N, Xp, kin, N, kin, M, dW, kin, pro=K.PRO_ENC, pro_s=stp.scale, pro_t=stp.shift)
             grads[4 * i] = dW.view(params[4 * i].shape)
-            grads[4 * i + 1] = K.colsum(cs, out=grad_buffer(params[4 * i + 1]))
+            grads[4 * i + 1] = bias.add(cs, grad_buffer(params[4 * i + 1]))
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
+        bias.flush()
         dx = None
         if ctx.needs_input_grad[1]:
             dx = torch.empty(M, Cin, device=dev)
