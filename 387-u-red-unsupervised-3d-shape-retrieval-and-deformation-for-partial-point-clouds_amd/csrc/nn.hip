@@ -666,12 +666,14 @@ __global__ __launch_bounds__(DCD_THREADS) void dcd_kernel(const float* __restric
 // ---- get_part regrouping backward (ured_part_rows_bwd) ---------------------------------------
 // Row-wise gather: each block covers rows_per_block output rows (C/V vector lanes per row), reads
 // the sorted-row gradient and the part-sum gradient of the row's sorted position once each (V
-// floats per lane) and writes the sum. HBM-bound: 2 reads + 1 write of R x C floats.
+// floats per lane) and writes the sum. HBM-bound: 2 reads + 1 write of R x C floats. `add`
+// (nullable, may be `out` itself) is another consumer's gradient of the same tensor, added last:
+// out = (ds + dsum) + add, the sum autograd would have formed.
 template <int V>
 __global__ __launch_bounds__(256) void part_rows_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ dsum,
                                                             const long long* __restrict__ inv,
                                                             const int* __restrict__ gid, int N, int C, long long rows,
-                                                            int rows_per_block, float* __restrict__ out) {
+                                                            int rows_per_block, const float* add, float* out) {
     const int per_row = C / V;
     const int lr = threadIdx.x / (per_row < 256 ? per_row : 256);
     if (lr >= rows_per_block) return;
@@ -687,10 +689,15 @@ __global__ __launch_bounds__(256) void part_rows_bwd_kernel(const float* __restr
                 const float4 u = reinterpret_cast<const float4*>(dsum + g * C)[c];
                 v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
             }
+            if (add) {
+                const float4 a = reinterpret_cast<const float4*>(add + r * C)[c];
+                v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+            }
             reinterpret_cast<float4*>(out + r * C)[c] = v;
         } else {
             float v = ds ? ds[s * C + c] : 0.f;
             if (dsum) v += dsum[g * C + c];
+            if (add) v += add[r * C + c];
             out[r * C + c] = v;
         }
     }
@@ -929,22 +936,27 @@ int ured_seg_aabb(const float* x, const int* off, int G, float* out, void* strea
 
 int ured_part_rows_bwd(const float* d_sorted, const float* d_sums, const long long* inv, const int* gid, int B, int N,
                        int C, float* out, void* stream) {
+    return ured_part_rows_bwd_add(d_sorted, d_sums, inv, gid, B, N, C, nullptr, out, stream);
+}
+
+int ured_part_rows_bwd_add(const float* d_sorted, const float* d_sums, const long long* inv, const int* gid, int B,
+                           int N, int C, const float* add, float* out, void* stream) {
     ured::clear_error();
     URED_REQUIRE(B >= 0 && N >= 0 && C >= 0, "ured_part_rows_bwd: negative size");
     if (B == 0 || N == 0 || C == 0) return 0;
     URED_REQUIRE(inv && gid && out, "ured_part_rows_bwd: null pointer");
     URED_REQUIRE((long long)B * N * C < (1LL << 40), "ured_part_rows_bwd: too large");
-    const bool vec = C % 4 == 0 && (((uintptr_t)out | (uintptr_t)d_sorted | (uintptr_t)d_sums) & 15) == 0;
+    const bool vec = C % 4 == 0 && (((uintptr_t)out | (uintptr_t)d_sorted | (uintptr_t)d_sums | (uintptr_t)add) & 15) == 0;
     const long long rows = (long long)B * N;
     const int per_row = vec ? C / 4 : C;
     const int rows_per_block = per_row >= 256 ? 1 : 256 / per_row;
     const unsigned grid = (unsigned)((rows + rows_per_block - 1) / rows_per_block);
     if (vec)
         hipLaunchKernelGGL(part_rows_bwd_kernel<4>, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_sorted, d_sums, inv,
-                           gid, N, C, rows, rows_per_block, out);
+                           gid, N, C, rows, rows_per_block, add, out);
     else
         hipLaunchKernelGGL(part_rows_bwd_kernel<1>, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_sorted, d_sums, inv,
-                           gid, N, C, rows, rows_per_block, out);
+                           gid, N, C, rows, rows_per_block, add, out);
     return ured::launch_status("ured_part_rows_bwd");
 }
 

@@ -51,7 +51,7 @@ from network.simple_encoder import TargetEncoder as simple_encoder  # noqa: E402
 from train_utils.load_sources import load_sources  # noqa: E402
 from train_utils.optimizer_dm import define_optimizer_dm_re_recon  # noqa: E402
 from ured_hip.kernels import RowWeights  # noqa: E402
-from ured_hip.ops import PartBounds, UniqueRows, build_parts, part_aabb, part_rows, upload  # noqa: E402
+from ured_hip.ops import PartBounds, UniqueRows, build_parts, part_aabb, part_rows, share_grad, upload  # noqa: E402
 
 MODULE_NAMES = ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "re_residual_net_full",
                 "src_encoder_all", "recon_decoder_src", "embedding_layer")
@@ -96,8 +96,9 @@ class ReInput:
         self.pp_sorted, self.part_mean, self.gid, self.off = pp_sorted, part_mean, gid, off
 
 
-def get_part(cfg, per_point_full, target_labels, x):
-    """engine/train.py:103-136 without host syncs. per_point_full [B, N, C].
+def get_part(cfg, per_point_full, target_labels, x, share=None):
+    """engine/train.py:103-136 without host syncs. per_point_full [B, N, C]; share: its
+    ured_hip.ops.SharedGrad slot, if any.
 
     Returns (target_part_f [B,P,C], None (the unused per-part feature lists), ReInput,
     mask_part [B,P], PartBatch (the part_x lists), param_def [B,P,6]).
@@ -105,7 +106,7 @@ def get_part(cfg, per_point_full, target_labels, x):
     B, N, C = per_point_full.shape
     P = cfg["MAX_NUM_PARTS"]
     parts = build_parts(target_labels, x, P)
-    pp_sorted, sums = part_rows(per_point_full, parts)
+    pp_sorted, sums = part_rows(per_point_full, parts, share)
     part_mean = sums / parts.counts.reshape(-1, 1).clamp(min=1).float()
     param_def = getattr(parts, "param_def", None)                      # indexed by label value (train.py:120)
     if param_def is None:
@@ -249,7 +250,8 @@ class TrainStep:
         src_points = get_source_points(src_labels, self.db) if uq is None else None
         codes, rec_u, pts_u, inv = self._source_branch(uq, src_points, src_sem_f, B, P, expand_rec=False)
         tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
-        target_part_f, _, re_in, mask_part, parts, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
+        pp, pp_share = share_grad(pp)      # get_part and recon_decoder_full sum pp's gradient in-kernel
+        target_part_f, _, re_in, mask_part, parts, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x, pp_share)
         codes = codes.view(B, P, -1)
         dside = self.deform_stream
         if dside is not None:
@@ -266,7 +268,7 @@ class TrainStep:
         else:
             params_full = M["param_decoder_full"](tcode, codes, None)
             out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
-        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
+        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N, share=pp_share).view(B, N, 3)
         re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
                                                          off=re_in.off).view(B, N, 3)
         if dside is not None:
@@ -320,7 +322,8 @@ class TrainStep:
         else:
             codes, recon_src_p = self._source_branch(uq, src_points, src_sem_f, B, P)
         tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
-        target_part_f, _, re_in, mask_part, part_x, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
+        pp, pp_share = share_grad(pp)      # get_part and recon_decoder_full sum pp's gradient in-kernel
+        target_part_f, _, re_in, mask_part, part_x, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x, pp_share)
         if side is not None:
             main.wait_stream(side)
             codes.record_stream(main)
@@ -346,7 +349,7 @@ class TrainStep:
         else:
             loss_d, out, params_full, knn_idx = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
                                                                     mask_part, target_part_f, src_labels)
-        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
+        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N, share=pp_share).view(B, N, 3)
         re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
                                                          off=re_in.off).view(B, N, 3)
         if dside is not None:

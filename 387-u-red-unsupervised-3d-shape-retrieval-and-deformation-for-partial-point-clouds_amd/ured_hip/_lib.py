@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libured_hip.so"
 # URED_LIB: an alternative build of the same ABI (A/B kernel experiments, tools/)
 LIB_PATH = os.environ.get("URED_LIB") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -29,6 +29,7 @@ _SIGNATURES = {
     "ured_nn_fwd_workspace": [_I, _I, _I, _I, _I, _I],
     "ured_seg_aabb": [_P, _P, _I, _P, _P],
     "ured_part_rows_bwd": [_P, _P, _P, _P, _I, _I, _I, _P, _P],
+    "ured_part_rows_bwd_add": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
     "ured_get_shape_fwd": [_P, _P, _I, _I, _P, _P],
     "ured_get_shape_bwd": [_P, _P, _I, _I, _P, _P],
     "ured_emd_workspace": [_I, _I],

@@ -261,7 +261,7 @@ class ResidualNetFn(Function):
 
     @staticmethod
     def forward(ctx, spec, pp, code, *params):
-        code_first, gidx, off, group_rows, training, bn_modules, rw = spec
+        code_first, gidx, off, group_rows, training, bn_modules, rw = spec[:7]
         pp = pp.contiguous()
         code = code.contiguous()
         M, Cp = pp.shape
@@ -311,7 +311,8 @@ class ResidualNetFn(Function):
 
     @staticmethod
     def backward(ctx, dout):
-        code_first, gidx, off, group_rows, training, bn_modules, rw = ctx.spec
+        code_first, gidx, off, group_rows, training, bn_modules, rw = ctx.spec[:7]
+        share = ctx.spec[7] if len(ctx.spec) > 7 else None     # ops.SharedGrad slot of pp
         states = ctx.states
         saved = ctx.saved_tensors
         pp, code = saved[:2]
@@ -376,6 +377,12 @@ class ResidualNetFn(Function):
         dpp = torch.empty(M, Cp, device=dev)
         K.gemm(M, Cp, W1.shape[0], dY, W1.shape[0], W1, ld1, dpp, Cp, b_kmajor=True, B_off=pp_off)
         sw.join()
+        if share is not None:        # pp's other consumer sums into this buffer (or already did)
+            if share.buf is None:
+                share.buf = dpp
+            else:
+                share.buf.view(M, Cp).add_(dpp)
+            dpp = None
         return (None, dpp, dcode) + tuple(grads)
 
 

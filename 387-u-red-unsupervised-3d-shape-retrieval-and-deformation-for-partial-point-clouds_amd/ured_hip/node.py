@@ -87,6 +87,14 @@ def _mat(t):
     return t.data_ptr(), t.stride(0)
 
 
+def _rows(g):
+    """g as a row-major 2-D view the node kernels read in place (any row stride >= its width,
+    unit column stride: e.g. a column slice of NodeFFNFn's [d first | d message]), else a copy."""
+    if g.dim() == 2 and g.stride(1) == 1 and g.stride(0) >= g.shape[1]:
+        return g
+    return g.contiguous()
+
+
 def node_gemm_desc(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, *, A2=None, sam2=0, sak2=0, k1=None, accumulate=False,
                    bias=None, rowbias=None, ldrb=0, rdiv=1, relu_out=False, gate=None, ldgate=0, R=None, ldR=0,
                    R_ncols=None, B2=None, sbk2=0, sbn2=0, n1=None):
@@ -276,7 +284,7 @@ class NodeLinearFn(Function):
     @staticmethod
     def backward(ctx, g):
         x, W, b = ctx.saved_tensors
-        g = g.contiguous()
+        g = _rows(g)
         dx = dW = db = None
         jobs = []
         if ctx.needs_input_grad[0]:
@@ -389,7 +397,7 @@ class NodeProjFn(Function):
         for i, gsz in enumerate(groups):
             w, b = rest[o:o + gsz], rest[o + gsz:o + 2 * gsz]
             o += 2 * gsz
-            g = gs[i].contiguous()
+            g = _rows(gs[i])
             x = xs[i]
             dx = torch.empty(x.shape, device=x.device)
             dW, aW, fW = _grad_rows(w)
@@ -445,7 +453,7 @@ class NodeFFNFn(Function):
     def backward(ctx, g):
         bnm, off, training = ctx.spec
         x, msg, W1, gamma, W2, Y1, act, mean, invstd, b1, beta, b2 = ctx.saved_tensors
-        g = g.contiguous()
+        g = _rows(g)
         M, C = x.shape
         dev = x.device
         dact = torch.empty(act.shape, device=dev)
@@ -501,7 +509,7 @@ class ParamDecoderFn(Function):
         glob, parts, W1, W2, h, b1, b2 = ctx.saved_tensors
         P = ctx.P
         B, Cg = glob.shape
-        g = g.contiguous()
+        g = _rows(g)
         dev = g.device
         dW2 = grad_buffer(W2)
         db2 = grad_buffer(b2)

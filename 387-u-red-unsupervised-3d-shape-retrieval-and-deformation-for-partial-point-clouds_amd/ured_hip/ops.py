@@ -9,6 +9,7 @@ PartBatch     : the ragged per-part view of a target batch that the reference
 build_parts   : computes a PartBatch with device ops only (no host sync).
 """
 import ctypes
+import os
 
 import torch
 from torch.autograd import Function
@@ -77,6 +78,49 @@ def permute_rows(x, perm, inv):
     return PermuteRowsFn.apply(x, perm, inv)
 
 
+class SharedGrad:
+    """The gradient of a tensor that several HIP Functions consume, summed by their kernels
+    instead of by autograd. share_grad(x) returns (x', slot); each consumer built with the slot
+    returns no gradient for x' and, in its backward, writes its gradient into slot.buf (the first
+    one to run) or accumulates into it (a later one: in its own kernel where it can, else one
+    add); ShareFn's backward — which autograd runs after every consumer of x' — hands slot.buf
+    on as x's gradient (plus any gradient x' received from ordinary consumers). Used for the
+    target per-point features pp, read by get_part's regrouping and the reconstruction decoder
+    (engine/train.py:240,250): one [B*N, C] pass less per step."""
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+
+class ShareFn(Function):
+    @staticmethod
+    def forward(ctx, x, slot):
+        ctx.slot, ctx.shape = slot, x.shape
+        ctx.set_materialize_grads(False)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        buf, ctx.slot.buf = ctx.slot.buf, None
+        if buf is None:
+            return g, None
+        buf = buf.view(ctx.shape)
+        return (buf if g is None else buf + g), None
+
+
+SHARE_GRAD = os.environ.get("URED_SHARE_GRAD", "1") != "0"     # A/B knob: 0 = autograd sums
+
+
+def share_grad(x):
+    """(x', SharedGrad) — see SharedGrad; (x, None) with URED_SHARE_GRAD=0."""
+    if not SHARE_GRAD:
+        return x, None
+    slot = SharedGrad()
+    y = ShareFn.apply(x, slot)
+    return y, slot
+
+
 class PartRowsFn(Function):
     """get_part's regrouping of per-point features (engine/train.py:103-136): x [B, N, C] ->
     (rows sorted by part label [B*N, C], per-part-slot sums [G, C]). Forward: one gather and one
@@ -84,12 +128,13 @@ class PartRowsFn(Function):
     take an index_select of the part gradients, an add and the inverse-permutation gather."""
 
     @staticmethod
-    def forward(ctx, x, perm, inv, off, gid):
+    def forward(ctx, x, perm, inv, off, gid, share=None):
         B, N, C = x.shape
         xs = torch.gather(x, 1, perm.unsqueeze(-1).expand(-1, -1, C)).reshape(B * N, C)
         sums = K.group_colsum(xs, C, off.shape[0] - 1, off=off)
         ctx.save_for_backward(inv, gid)
         ctx.shape = (B, N, C)
+        ctx.share = share
         return xs, sums
 
     @staticmethod
@@ -100,16 +145,24 @@ class PartRowsFn(Function):
         dg = None if d_sums is None else d_sums.contiguous()
         if inv.dtype != torch.int64 or gid.dtype != torch.int32:
             raise TypeError("part_rows: inv must be int64 and gid int32")
-        out = torch.empty(B, N, C, device=inv.device)
-        _lib.call("ured_part_rows_bwd", _lib.ptr(ds), _lib.ptr(dg), _lib.ptr(inv.contiguous()), _lib.ptr(gid.contiguous()),
-                  B, N, C, _lib.ptr(out), _lib.stream_of(out))
-        return out, None, None, None, None
+        sh = ctx.share
+        acc = None if sh is None else sh.buf        # another consumer's gradient of x: add in the kernel
+        out = torch.empty(B, N, C, device=inv.device) if acc is None else acc
+        if acc is not None and (not acc.is_contiguous() or acc.numel() != B * N * C):
+            raise ValueError("part_rows: shared gradient buffer must be a contiguous [B*N, C] tensor")
+        _lib.call("ured_part_rows_bwd_add", _lib.ptr(ds), _lib.ptr(dg), _lib.ptr(inv.contiguous()),
+                  _lib.ptr(gid.contiguous()), B, N, C, _lib.ptr(acc), _lib.ptr(out), _lib.stream_of(out))
+        if sh is not None:
+            sh.buf = out
+            return None, None, None, None, None, None
+        return out, None, None, None, None, None
 
 
-def part_rows(x, parts):
-    """(x regrouped by part [B*N, C], per-part-slot sums [B*P, C]) for a PartBatch."""
+def part_rows(x, parts, share=None):
+    """(x regrouped by part [B*N, C], per-part-slot sums [B*P, C]) for a PartBatch; `share`: a
+    SharedGrad slot of x (its gradient is then summed there, see SharedGrad)."""
     _lib.require_device(x)
-    return PartRowsFn.apply(x, parts.perm, parts.inv_perm, parts.off, parts.gid)
+    return PartRowsFn.apply(x, parts.perm, parts.inv_perm, parts.off, parts.gid, share)
 
 
 def segment_sum(x, off, gid):

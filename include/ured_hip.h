@@ -40,7 +40,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 5   /* 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
+#define URED_ABI_VERSION 6   /* 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
@@ -110,6 +110,12 @@ int ured_seg_aabb(const float* x, const int* off, int G, float* out, void* strea
  * Either gradient may be NULL (zero). One pass: replaces an index_select, a gather and an add. */
 int ured_part_rows_bwd(const float* d_sorted, const float* d_sums, const long long* inv, const int* gid, int B, int N,
                        int C, float* out, void* stream);
+/* The same plus `add` [R,C] (may be NULL, or `out` itself: in-place accumulation): out = (d_sorted
+ * + d_sums) + add, where add is another consumer's gradient of the same per-point features (the
+ * reconstruction decoder's input gradient, engine/train.py:240,250): the sum autograd would form
+ * in a separate pass (ABI 6). */
+int ured_part_rows_bwd_add(const float* d_sorted, const float* d_sums, const long long* inv, const int* gid, int B,
+                           int N, int C, const float* add, float* out, void* stream);
 
 /* ---------------- EMD (auction algorithm) ---------------- */
 /* Approximate EMD matching of xyz1 [b,n,3] to xyz2 [b,n,3] (reference emd.forward,
