@@ -23,8 +23,9 @@ if "seq" in sys.argv:
     orig = node.launch
     node.launch = lambda *ds: [orig(d) for d in ds]
 if "noproj" in sys.argv:    # each projection group as its own launch
-    agn.node_proj = lambda xs, ws, bs: tuple(node.node_proj((x,), [w], [b]) for x, w, b in zip(xs, ws, bs)) \
-        if len(xs) > 1 else node.node_proj(xs, ws, bs)
+    agn.node_proj = lambda xs, ws, bs, sh=None: tuple(node.node_proj((x,), [w], [b], (s,)) for x, w, b, s in
+                                                      zip(xs, ws, bs, sh or (None,) * len(xs))) \
+        if len(xs) > 1 else node.node_proj(xs, ws, bs, sh)
 if "noffn" in sys.argv:
     agn.ResidualAttentionMessagePropagation._node_ffn_ok = lambda self: False
 if "nopd" in sys.argv:
