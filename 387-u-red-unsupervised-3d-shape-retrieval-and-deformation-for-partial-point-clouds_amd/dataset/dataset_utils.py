@@ -61,10 +61,11 @@ def _index(source_labels, db):
     return torch.where(idx < 0, idx + db.num_sources, idx)   # python negative indexing, dataset_utils.py:800-805
 
 
-def get_source_info(source_labels, db, use_connectivity=False):
-    """-> (mats [B,P,3n,6], default_params [B,P,6], sem_idx [B,P]) gathered on the device."""
+def get_source_info(source_labels, db, use_connectivity=False, want=(True, True, True)):
+    """-> (mats [B,P,3n,6], default_params [B,P,6], sem_idx [B,P]) gathered on the device;
+    `want` skips the gathers of fields the caller does not read (None in their place)."""
     idx = _index(source_labels, db)
-    return db.mats[idx], db.default_param[idx], db.sem[idx]
+    return tuple(t[idx] if w else None for t, w in zip((db.mats, db.default_param, db.sem), want))
 
 
 def get_source_points(source_labels, db, device=None):

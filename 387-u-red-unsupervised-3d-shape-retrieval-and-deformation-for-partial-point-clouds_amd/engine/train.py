@@ -241,7 +241,8 @@ class TrainStep:
         B, N, _ = x.shape
         src_labels = batch["src_labels"]
         uq = batch.get("src_unique") if cfg.get("unique_sources", True) else None
-        mats, _, src_sem_idx = get_source_info(src_labels, self.db)
+        # the unique-source path embeds the distinct parts' semantics itself (_source_branch)
+        mats, _, src_sem_idx = get_source_info(src_labels, self.db, want=(True, False, uq is None))
         emb = M["embedding_layer"]
         with torch.no_grad():          # the embedding is not trained (optimizer_dm.py:83)
             src_sem_f = emb(src_sem_idx) if uq is None else None

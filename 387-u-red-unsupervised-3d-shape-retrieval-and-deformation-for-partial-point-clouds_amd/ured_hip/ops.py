@@ -130,7 +130,15 @@ class PartRowsFn(Function):
     @staticmethod
     def forward(ctx, x, perm, inv, off, gid, share=None):
         B, N, C = x.shape
-        xs = torch.gather(x, 1, perm.unsqueeze(-1).expand(-1, -1, C)).reshape(B * N, C)
+        x = x.contiguous()
+        if perm.dtype != torch.int64 or gid.dtype != torch.int32:
+            raise TypeError("part_rows: perm must be int64 and gid int32")
+        # the row gather xs[b*N + i] = x[b, perm[b, i]] is the backward kernel's gather with the
+        # permutation in place of its inverse and no part-sum term (one float4 row copy per lane,
+        # where torch.gather reads an int64 index per element)
+        xs = torch.empty(B * N, C, device=x.device)
+        _lib.call("ured_part_rows_bwd", _lib.ptr(x), None, _lib.ptr(perm.contiguous()), _lib.ptr(gid.contiguous()),
+                  B, N, C, _lib.ptr(xs), _lib.stream_of(xs))
         sums = K.group_colsum(xs, C, off.shape[0] - 1, off=off)
         ctx.save_for_backward(inv, gid)
         ctx.shape = (B, N, C)
