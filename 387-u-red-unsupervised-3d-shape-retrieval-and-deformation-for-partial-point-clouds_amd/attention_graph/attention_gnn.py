@@ -23,7 +23,8 @@ from . import get_attention_mechanism
 from .attention import softmax_attention
 from .attention_utils import FeedForwardNet_norm, conv1x1
 
-_ATTN_PAIR = os.environ.get("URED_ATTN_PAIR", "1") != "0"     # A/B knob
+# opt-in, with URED_SHARE_GRAD (ured_hip/ops.py SHARE_GRAD: an 8-rank fault not yet explained)
+_ATTN_PAIR = os.environ.get("URED_ATTN_PAIR", "0") == "1"
 
 
 class MultiheadAttention(nn.Module):

@@ -109,11 +109,16 @@ class ShareFn(Function):
         return (buf if g is None else buf + g), None
 
 
-SHARE_GRAD = os.environ.get("URED_SHARE_GRAD", "1") != "0"     # A/B knob: 0 = autograd sums
+# Opt-in (URED_SHARE_GRAD=1): +0.5 % on the config-2 step, bitwise-tested, but the 8-rank
+# data-parallel test (tests/test_dp_configs_gpu.py config 5: eight processes on one GPU, gloo,
+# bucketed all-reduce from backward hooks) hit a GPU memory fault 2 of 2 times with it (and
+# URED_ATTN_PAIR) on, 0 of 2 with both off, and passed with kernels serialised
+# (AMD_SERIALIZE_KERNEL=3): an ordering hazard not yet found, so it stays off by default.
+SHARE_GRAD = os.environ.get("URED_SHARE_GRAD", "0") == "1"
 
 
 def share_grad(x):
-    """(x', SharedGrad) — see SharedGrad; (x, None) with URED_SHARE_GRAD=0."""
+    """(x', SharedGrad) — see SharedGrad; (x, None) unless URED_SHARE_GRAD=1 (see SHARE_GRAD)."""
     if not SHARE_GRAD:
         return x, None
     slot = SharedGrad()

@@ -101,7 +101,8 @@ def _worker(rank, world, port, bs, npts, q):
         res["losses"] = losses
         torch.cuda.synchronize()
     except Exception as e:                          # reported to the parent, which fails the test
-        res["error"] = repr(e)
+        import traceback
+        res["error"] = repr(e) + "\n" + traceback.format_exc()[-3000:]
     finally:
         q.put(res)
         dist.destroy_process_group()

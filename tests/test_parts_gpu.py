@@ -91,12 +91,14 @@ def test_part_rows_matches_separate_ops(dev, B, N, P, C, kmax):
 
 
 @pytest.mark.parametrize("C", [512, 6])
-def test_part_rows_shared_gradient(dev, C):
+def test_part_rows_shared_gradient(dev, C, monkeypatch):
     """pp read by get_part's regrouping and by another consumer (the reconstruction decoder),
     its two gradients summed by the kernels through a SharedGrad slot (ured_part_rows_bwd_add,
     in place) == autograd's sum of the two, bitwise, whichever consumer's backward runs first;
     a gradient the shared tensor also receives from an ordinary op is added too."""
+    from ured_hip import ops
     from ured_hip.ops import build_parts, part_rows, share_grad
+    monkeypatch.setattr(ops, "SHARE_GRAD", True)      # opt-in in the product (ops.SHARE_GRAD)
     B, N, P = 4, 300, 16
     g = torch.Generator().manual_seed(C)
     x = torch.randn(B, N, C, generator=g).to(dev)
