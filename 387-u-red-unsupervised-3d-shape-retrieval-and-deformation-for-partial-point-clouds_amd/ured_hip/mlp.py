@@ -306,6 +306,8 @@ class ResidualNetFn(Function):
         K.gemm(M, W4.shape[0], kin, h, kin, W4, W4.shape[1], out, W4.shape[0], pro_a=K.PRO_RES,
                pro_s=st.scale, pro_t=st.shift, bias=params[13])
         ctx.spec, ctx.states = spec, states
+        if len(spec) > 7 and spec[7] is not None:
+            spec[7].register()              # ops.SharedGrad slot of pp
         ctx.save_for_backward(pp, code, *Ys, *params)
         return out
 
@@ -382,7 +384,7 @@ class ResidualNetFn(Function):
                 share.buf = dpp
             else:
                 share.buf.view(M, Cp).add_(dpp)
-            dpp = None
+            dpp = share.finish((M, Cp))
         return (None, dpp, dcode) + tuple(grads)
 
 

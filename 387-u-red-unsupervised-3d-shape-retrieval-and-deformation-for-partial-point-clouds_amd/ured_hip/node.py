@@ -385,6 +385,9 @@ class NodeProjFn(Function):
         n = len(groups)
         xs, rest = tensors[:n], tensors[n:]
         ctx.shares = shares
+        for sh in shares:
+            if sh is not None:
+                sh.register()
         _lib.require_device(*xs)
         Ws, bs, o = [], [], 0
         for gsz in groups:
@@ -419,9 +422,10 @@ class NodeProjFn(Function):
             db, ab, fb = _grad_rows(b)
             jobs += [dgrad_desc(g, _stack_rows(w), dx, accumulate=adx), wgrad_desc(g, x, dW, accumulate=aW),
                      colsum_desc(g, db, accumulate=ab)]
-            dxs.append(dx if ctx.shares[i] is None else None)
+            dxs.append(dx)
             fins.append((fW, fb))
         launch(*jobs)
+        dxs = [dx if sh is None else sh.finish(dx.shape) for dx, sh in zip(dxs, ctx.shares)]
         out = [None, None] + dxs
         for fW, fb in fins:
             out += fW() + fb()
@@ -447,6 +451,8 @@ class NodeFFNFn(Function):
     @staticmethod
     def forward(ctx, spec, x, msg, R, W1, b1, gamma, beta, W2, b2):
         bnm, off, training = spec[:3]
+        if len(spec) > 3 and spec[3] is not None:
+            spec[3].register()
         ctx.res_is_x = R is None
         R = x if R is None else R
         M, C = x.shape
@@ -496,7 +502,7 @@ class NodeFFNFn(Function):
             launch(wgrad_desc(dY1, x, dW1, accumulate=aW1, x2=msg),
                    dgrad_desc(dY1, W1[:, :C], dxs, R=R, R_ncols=C, accumulate=adx),
                    dgrad_desc(dY1, W1[:, C:], dmsg), colsum_desc(dY1, db1, accumulate=ab1))
-            dx = None
+            dx = share.finish(x.shape)
         return (None, dx, dmsg, (None if ctx.res_is_x else g),
                 *(None if acc else t for t, acc in ((dW1, aW1), (db1, ab1), (dgamma, ag), (dbeta, abe), (dW2, aW2),
                                                     (db2, ab2))))

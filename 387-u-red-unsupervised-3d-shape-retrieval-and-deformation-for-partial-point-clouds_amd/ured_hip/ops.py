@@ -87,10 +87,24 @@ class SharedGrad:
     on as x's gradient (plus any gradient x' received from ordinary consumers). Used for the
     target per-point features pp, read by get_part's regrouping and the reconstruction decoder
     (engine/train.py:240,250): one [B*N, C] pass less per step."""
-    __slots__ = ("buf",)
+    __slots__ = ("buf", "expected", "done")
 
     def __init__(self):
-        self.buf = None
+        self.buf, self.expected, self.done = None, 0, 0
+
+    def register(self):
+        """A consumer's forward: one more backward will write into this slot."""
+        self.expected += 1
+
+    def finish(self, shape):
+        """A consumer's backward, after writing: the finished sum (viewed as `shape`) for the last
+        registered consumer to hand autograd as its input gradient — so ShareFn's node receives a
+        defined gradient and runs on the device queue — else None."""
+        self.done += 1
+        if self.done < self.expected or self.buf is None:
+            return None
+        b, self.buf = self.buf, None
+        return b.view(shape)
 
 
 class ShareFn(Function):
@@ -148,6 +162,8 @@ class PartRowsFn(Function):
         ctx.save_for_backward(inv, gid)
         ctx.shape = (B, N, C)
         ctx.share = share
+        if share is not None:
+            share.register()
         return xs, sums
 
     @staticmethod
@@ -167,7 +183,7 @@ class PartRowsFn(Function):
                   _lib.ptr(gid.contiguous()), B, N, C, _lib.ptr(acc), _lib.ptr(out), _lib.stream_of(out))
         if sh is not None:
             sh.buf = out
-            return None, None, None, None, None, None
+            return sh.finish((B, N, C)), None, None, None, None, None
         return out, None, None, None, None, None
 
 
