@@ -10,21 +10,15 @@ kernel each way (ured_hip.attn), out_proj as a node GEMM, and the FeedForwardNet
 BatchNorm kernel, the concatenation [x, message] read in place. `forward` keeps the
 reference's channel-first signature for drop-in callers.
 """
-import os
-
 import torch
 import torch.nn as nn
 
-from ured_hip.attn import cross_attention, self_attention, self_attention_pair
+from ured_hip.attn import cross_attention, self_attention
 from ured_hip.node import node_ffn, node_linear, node_proj
-from ured_hip.ops import share_grad
 
 from . import get_attention_mechanism
 from .attention import softmax_attention
 from .attention_utils import FeedForwardNet_norm, conv1x1
-
-# opt-in, with URED_SHARE_GRAD (ured_hip/ops.py SHARE_GRAD: an 8-rank fault not yet explained)
-_ATTN_PAIR = os.environ.get("URED_ATTN_PAIR", "0") == "1"
 
 
 class MultiheadAttention(nn.Module):
@@ -56,22 +50,21 @@ class MultiheadAttention(nn.Module):
     def _w(conv):
         return conv.weight.view(conv.weight.shape[0], -1)
 
-    def forward_nodes(self, xq, xkv=None, q_share=None, kv_share=None):
+    def forward_nodes(self, xq, xkv=None):
         """Node-major [B, n, C] query nodes and [B, m, C] key/value nodes (None: self-attention)
-        -> message [B, n, C]; *_share: SharedGrad slots of xq / xkv (ured_hip/ops.py)."""
+        -> message [B, n, C]."""
         if self.attention_func is not softmax_attention:
             raise NotImplementedError("node-major path implements the softmax attention only")
         q_, k_, v_ = self.in_proj_q, self.in_proj_k, self.in_proj_v
         B, n, C = xq.shape
         if xkv is None:
             qkv = node_proj((xq.reshape(B * n, C),), [(self._w(q_), self._w(k_), self._w(v_))],
-                            [(q_.bias, k_.bias, v_.bias)], (q_share,))
+                            [(q_.bias, k_.bias, v_.bias)])
             out = self_attention(qkv.view(B, n, 3 * C), self.num_heads)
         else:
             m = xkv.shape[1]
             q, kv = node_proj((xq.reshape(B * n, C), xkv.reshape(B * m, C)),
-                              [(self._w(q_),), (self._w(k_), self._w(v_))], [(q_.bias,), (k_.bias, v_.bias)],
-                              (q_share, kv_share))
+                              [(self._w(q_),), (self._w(k_), self._w(v_))], [(q_.bias,), (k_.bias, v_.bias)])
             out = cross_attention(q.view(B, n, C), kv.view(B, m, 2 * C), self.num_heads)
         return node_linear(out.reshape(B * n, C), self._w(self.out_proj), self.out_proj.bias).view(B, n, C)
 
@@ -88,19 +81,16 @@ class ResidualAttentionMessagePropagation(nn.Module):
         first = desc_q - message if self.use_offset else desc_q
         return desc_q + self.fc(torch.cat([first, message], dim=1))
 
-    def forward_nodes(self, xq, xkv=None, q_share=None, kv_share=None):
-        """q_share / kv_share: SharedGrad slots of xq / xkv (the layer's consumers of a node set
-        sum its gradient in their GEMMs, ured_hip/ops.py); only with the node FFN path."""
+    def forward_nodes(self, xq, xkv=None):
         if not self._node_ffn_ok():
-            assert q_share is None and kv_share is None
             message = self.mha.forward_nodes(xq, xkv)
             first = xq - message if self.use_offset else xq
             return xq + self.fc.forward_nodes(torch.cat([first, message], dim=-1))
-        message = self.mha.forward_nodes(xq, xkv, q_share, kv_share)
+        message = self.mha.forward_nodes(xq, xkv)
         B, n, C = xq.shape
         x2, m2 = xq.reshape(B * n, C), message.reshape(B * n, C)
         first, R = (x2 - m2, x2) if self.use_offset else (x2, None)
-        return node_ffn(self.fc, first, m2, R, (0, B * n), None if self.use_offset else q_share).view(B, n, C)
+        return node_ffn(self.fc, first, m2, R, (0, B * n)).view(B, n, C)
 
     def _node_ffn_ok(self):
         return self.fc.use_norm == "use_bn" and len(self.fc) == 4
@@ -117,19 +107,15 @@ class ResidualAttentionMessagePropagation(nn.Module):
         B, n0, C = x0.shape
         n1 = x1.shape[1]
         R0, R1 = B * n0, B * n1
-        X, sX = share_grad(torch.cat([x0.reshape(R0, C), x1.reshape(R1, C)]))    # read by q|k|v and the FFN
+        X = torch.cat([x0.reshape(R0, C), x1.reshape(R1, C)])
         q_, k_, v_ = mha.in_proj_q, mha.in_proj_k, mha.in_proj_v
-        qkv = node_proj((X,), [(mha._w(q_), mha._w(k_), mha._w(v_))], [(q_.bias, k_.bias, v_.bias)], (sX,))
-        if _ATTN_PAIR:
-            o = self_attention_pair(qkv, B, n0, n1, mha.num_heads)     # both sets, one output buffer
-        else:
-            q0, q1 = qkv.split([R0, R1])
-            o = torch.cat([self_attention(q0.view(B, n0, -1), mha.num_heads).reshape(R0, C),
-                           self_attention(q1.view(B, n1, -1), mha.num_heads).reshape(R1, C)])
+        qkv = node_proj((X,), [(mha._w(q_), mha._w(k_), mha._w(v_))], [(q_.bias, k_.bias, v_.bias)])
+        q0, q1 = qkv.split([R0, R1])
+        o = torch.cat([self_attention(q0.view(B, n0, -1), mha.num_heads).reshape(R0, C),
+                       self_attention(q1.view(B, n1, -1), mha.num_heads).reshape(R1, C)])
         message = node_linear(o, mha._w(mha.out_proj), mha.out_proj.bias)
         first, R = (X - message, X) if self.use_offset else (X, None)
-        out0, out1 = node_ffn(self.fc, first, message, R, (0, R0, R0 + R1),
-                              None if self.use_offset else sX).split([R0, R1])
+        out0, out1 = node_ffn(self.fc, first, message, R, (0, R0, R0 + R1)).split([R0, R1])
         return out0.view(B, n0, C), out1.view(B, n1, C)
 
 
@@ -155,16 +141,8 @@ class DescriptorsCrossAttention(nn.Module):
         return desc0, self.module(desc1, desc0)
 
     def forward_nodes(self, desc0, desc1):
-        m = self.module
-        if not m._node_ffn_ok() or m.mha.attention_func is not softmax_attention:
-            desc0 = m.forward_nodes(desc0, desc1)
-            return desc0, m.forward_nodes(desc1, desc0)
-        # desc0 is read by update 0's q projection and FFN, desc1 by update 0's k|v projection and
-        # update 1's q projection and FFN: each set's gradient is summed in those GEMMs
-        d0, s0 = share_grad(desc0)
-        d1, s1 = share_grad(desc1)
-        desc0 = m.forward_nodes(d0, d1, q_share=s0, kv_share=s1)
-        return desc0, m.forward_nodes(d1, desc0, q_share=s1)
+        desc0 = self.module.forward_nodes(desc0, desc1)     # the updated desc0 feeds desc1's update
+        return desc0, self.module.forward_nodes(desc1, desc0)
 
 
 class GraphAttentionNet(nn.Module):

@@ -25,8 +25,11 @@ REFERENCE_READS = {
     "use_symmetry_loss", "use_residuals_reg", "init_p_m_loss", "use_recon",
     # pseudo-labels (dataset/dataset_utils.py:1101-1143)
     "filter_threshold", "cl_k",
+    # loader: "mode" != "train" -> batch size 2, dataset order (engine/train.py:160-165,174;
+    # engine/train.py loader_batching)
+    "mode",
     # data location (partnet_dataset, load_sources): inert with "synthetic": true
-    "base_dir", "middle_name", "category", "num_source", "mode", "num_workers", "src_connectivity",
+    "base_dir", "middle_name", "category", "num_source", "num_workers", "src_connectivity",
     # inference (engine/vis.py)
     "top_k",
 }
@@ -36,8 +39,8 @@ REFERENCE_UNREAD = {
 }
 EXTRA = {
     "synthetic", "seed", "num_points", "parts", "num_targets", "iters_per_epoch", "pseudo_labels",
-    "unique_sources", "flat_adam", "fused_adam", "cuda_graph", "stream_overlap", "deform_overlap",
-    "log_every", "compute_connectivity", "differentiable_gather", "sync_bn", "loss_head", "dist_backend",
+    "unique_sources", "flat_adam", "fused_adam", "cuda_graph",
+    "log_every", "compute_connectivity", "src_connectivity_plane", "differentiable_gather", "sync_bn", "loss_head", "dist_backend",
 }
 
 TRAIN_REQUIRED = ("source_latent_dim", "target_latent_dim", "sem_latent_dim", "MAX_NUM_PARTS", "device",

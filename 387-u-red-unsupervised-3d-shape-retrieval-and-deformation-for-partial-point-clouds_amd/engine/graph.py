@@ -8,7 +8,9 @@ are built on the device or from host labels before the step), so it is captured 
 
   graph "fwd_bwd"[key] : grads.zero_() + forward + backward
   eager                : reduce_gradients()      (RCCL bucketed all-reduce when world > 1)
-  graph "update"       : clip_grad_norm_ x6 + Adam (capturable)
+  graph "update"       : clip_grad_norm_ x6 + Adam (capturable); FlatAdam reads the learning
+                         rate from a device scalar, torch's optimizers get the update graph
+                         re-captured when a scheduler changes the lr
 
 key = (the batch's padded distinct-source-part count (UniqueRows with a bucket; None when the
 batch encodes every slot), the residual-loss gate `epoch > init_p_m_loss`): one forward/backward
@@ -58,12 +60,6 @@ def _detached(T):
 
 class GraphedStep:
     def __init__(self, inner, example_batch=None, warmup=0, max_graphs=6):
-        import torch.distributed as dist
-        if (dist.is_initialized() and dist.get_world_size() > 1
-                and (getattr(inner, "side_stream", None) is not None or getattr(inner, "deform_stream", None) is not None)):
-            # a capture segment must end with every forked stream joined; the side-stream forms
-            # issue the contrastive all_gather on their side stream
-            raise NotImplementedError("graph replay with world > 1: not with stream_overlap / deform_overlap")
         self.inner = inner
         self.max_graphs = max_graphs
         self.graphs = OrderedDict()       # key -> (static batch, graph, loss dict)
@@ -131,6 +127,7 @@ class GraphedStep:
         return _detached(T)
 
     def _capture(self, key, batch, epoch):
+        self.captures = getattr(self, "captures", 0) + 1
         static = _clone_batch(batch)
         torch.cuda.synchronize()
         gc.collect()
@@ -163,13 +160,24 @@ class GraphedStep:
         T = _detached(T)
         del loss
         if self.g_update is None:
-            gu = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gu):
-                self.inner.clip_and_step()
-            self.g_update = gu
+            self._capture_update()
         self.graphs[key] = (static, cap, T)
         while len(self.graphs) > self.max_graphs:
             self.graphs.popitem(last=False)
+
+    def _lrs(self):
+        return tuple(float(g["lr"]) for g in self.inner.optimizer.param_groups)
+
+    def _capture_update(self):
+        """The update graph: clip + optimizer step. FlatAdam reads its learning rate from a device
+        scalar (sync_lr before each replay); torch's optimizers bake the float lr into the captured
+        kernels, so their graph is re-captured whenever a scheduler has changed it."""
+        gu = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gu):
+            self.inner.clip_and_step()
+        self.g_update = gu
+        self._update_lrs = self._lrs()
+        self.update_captures = getattr(self, "update_captures", 0) + 1
 
     def step(self, batch, epoch=0):
         k = self.key(batch, epoch)
@@ -199,5 +207,7 @@ class GraphedStep:
         sync = getattr(self.inner.optimizer, "sync_lr", None)
         if sync is not None:                 # FlatAdam reads lr from a device scalar
             sync()
+        elif self._lrs() != self._update_lrs:
+            self._capture_update()           # lr baked into the captured kernels: re-capture
         self.g_update.replay()
         return T

@@ -51,7 +51,7 @@ from network.simple_encoder import TargetEncoder as simple_encoder  # noqa: E402
 from train_utils.load_sources import load_sources  # noqa: E402
 from train_utils.optimizer_dm import define_optimizer_dm_re_recon  # noqa: E402
 from ured_hip.kernels import RowWeights  # noqa: E402
-from ured_hip.ops import PartBounds, UniqueRows, build_parts, part_aabb, part_rows, share_grad, upload  # noqa: E402
+from ured_hip.ops import PartBounds, UniqueRows, build_parts, part_aabb, part_rows, upload  # noqa: E402
 
 MODULE_NAMES = ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "re_residual_net_full",
                 "src_encoder_all", "recon_decoder_src", "embedding_layer")
@@ -96,9 +96,8 @@ class ReInput:
         self.pp_sorted, self.part_mean, self.gid, self.off = pp_sorted, part_mean, gid, off
 
 
-def get_part(cfg, per_point_full, target_labels, x, share=None):
-    """engine/train.py:103-136 without host syncs. per_point_full [B, N, C]; share: its
-    ured_hip.ops.SharedGrad slot, if any.
+def get_part(cfg, per_point_full, target_labels, x):
+    """engine/train.py:103-136 without host syncs. per_point_full [B, N, C].
 
     Returns (target_part_f [B,P,C], None (the unused per-part feature lists), ReInput,
     mask_part [B,P], PartBatch (the part_x lists), param_def [B,P,6]).
@@ -106,7 +105,7 @@ def get_part(cfg, per_point_full, target_labels, x, share=None):
     B, N, C = per_point_full.shape
     P = cfg["MAX_NUM_PARTS"]
     parts = build_parts(target_labels, x, P)
-    pp_sorted, sums = part_rows(per_point_full, parts, share)
+    pp_sorted, sums = part_rows(per_point_full, parts)
     part_mean = sums / parts.counts.reshape(-1, 1).clamp(min=1).float()
     param_def = getattr(parts, "param_def", None)                      # indexed by label value (train.py:120)
     if param_def is None:
@@ -127,27 +126,16 @@ class TrainStep:
         self.np_per_part = db.points.shape[1]
         dev = torch.device(device or cfg["device"])
         self._zflip = torch.tensor([1.0, 1.0, -1.0], device=dev)
-        self.side_stream = (torch.cuda.Stream(device=dev)
-                            if dev.type == "cuda" and cfg.get("stream_overlap", False) else None)
-        self.deform_stream = (torch.cuda.Stream(device=dev)
-                              if dev.type == "cuda" and cfg.get("deform_overlap", False) else None)
         # the fused HIP loss head (ured_hip/losshead.py); False: the composed torch + NN-launch form
-        self.loss_head = dev.type == "cuda" and cfg.get("loss_head", True) and not cfg.get("stream_overlap", False)
+        self.loss_head = dev.type == "cuda" and cfg.get("loss_head", True)
         # optional SyncBN (ured_hip/syncbn.py): global-batch BN statistics over the ranks
         import torch.distributed as dist
         self.sync_bn = bool(cfg.get("sync_bn", False)) and dist.is_initialized() and dist.get_world_size() > 1
         if self.sync_bn:
             if dev.type != "cuda":
                 raise NotImplementedError("sync_bn: the HIP BatchNorm path only (a CUDA device)")
-            if self.side_stream is not None or self.deform_stream is not None:
-                raise NotImplementedError("sync_bn: its collectives need one stream order (no stream_overlap / "
-                                          "deform_overlap)")
         if dev.type == "cuda":       # process-wide: the last step constructed decides
-            from ured_hip import sidework, syncbn
-            if self.side_stream is not None or self.deform_stream is not None:
-                # the chains' weight-gradient side stream is not nested inside these side streams
-                # (a graph capture of that nesting crashed the HIP runtime on MI355X)
-                sidework.MODE = 0
+            from ured_hip import syncbn
             if self.sync_bn:
                 syncbn.enable()
             else:
@@ -251,31 +239,13 @@ class TrainStep:
         src_points = get_source_points(src_labels, self.db) if uq is None else None
         codes, rec_u, pts_u, inv = self._source_branch(uq, src_points, src_sem_f, B, P, expand_rec=False)
         tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
-        pp, pp_share = share_grad(pp)      # get_part and recon_decoder_full sum pp's gradient in-kernel
-        target_part_f, _, re_in, mask_part, parts, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x, pp_share)
+        target_part_f, _, re_in, mask_part, parts, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
         codes = codes.view(B, P, -1)
-        dside = self.deform_stream
-        if dside is not None:
-            # DeformNet + get_shape (latency-bound small kernels) on their own stream, overlapping
-            # the GEMM-bound residual / reconstruction nets (autograd runs each node's backward on
-            # its forward stream)
-            main = torch.cuda.current_stream(x.device)
-            dside.wait_stream(main)
-            for t in (tcode, codes, mats, param_def):
-                t.record_stream(dside)
-            with torch.cuda.stream(dside):
-                params_full = M["param_decoder_full"](tcode, codes, None)
-                out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
-        else:
-            params_full = M["param_decoder_full"](tcode, codes, None)
-            out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
-        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N, share=pp_share).view(B, N, 3)
+        params_full = M["param_decoder_full"](tcode, codes, None)
+        out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
+        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
         re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
                                                          off=re_in.off).view(B, N, 3)
-        if dside is not None:
-            main.wait_stream(dside)
-            out.record_stream(main)
-            params_full.record_stream(main)
         param = regularization_param(params_full, mask_part) if cfg.get("use_param_loss", 0.0) > 0.0 else None
         contrast_ext = None
         if get_world_size() > 1 and cfg.get("use_contrast_loss", 0.0) > 0.0:
@@ -309,56 +279,16 @@ class TrainStep:
             tgt_sem_f = emb(batch["tgt_sem"])
         src_points = get_source_points(src_labels, self.db)
         uq = batch.get("src_unique") if cfg.get("unique_sources", True) else None
-        side = self.side_stream
-        if side is not None:
-            # the source branch (encoder + recon_decoder_src, forward and — autograd runs each
-            # node on its forward stream — backward) overlaps the target branch: each fills the
-            # other's GEMM tails and small-kernel gaps
-            main = torch.cuda.current_stream(x.device)
-            side.wait_stream(main)
-            src_points.record_stream(side)      # main-stream tensors read by the side stream
-            src_sem_f.record_stream(side)
-            with torch.cuda.stream(side):
-                codes, recon_src_p = self._source_branch(uq, src_points, src_sem_f, B, P)
-        else:
-            codes, recon_src_p = self._source_branch(uq, src_points, src_sem_f, B, P)
+        codes, recon_src_p = self._source_branch(uq, src_points, src_sem_f, B, P)
         tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
-        pp, pp_share = share_grad(pp)      # get_part and recon_decoder_full sum pp's gradient in-kernel
-        target_part_f, _, re_in, mask_part, part_x, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x, pp_share)
-        if side is not None:
-            main.wait_stream(side)
-            codes.record_stream(main)
-            recon_src_p.record_stream(main)
+        target_part_f, _, re_in, mask_part, part_x, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
         codes = codes.view(B, P, -1)
         T = {}
-        dside = self.deform_stream
-        if dside is not None:
-            # DeformNet + get_shape + the chamfer / contrast / symmetry losses are hundreds of
-            # latency-bound small kernels; on their own stream they (and, autograd running each
-            # node on its forward stream, their backward) overlap the GEMM-bound residual and
-            # reconstruction nets of the main stream
-            main = torch.cuda.current_stream(x.device)
-            dside.wait_stream(main)
-            for t in (tcode, codes, mats, param_def, x, target_part_f, mask_part, src_labels):
-                t.record_stream(dside)
-            for t in vars(part_x).values():
-                if torch.is_tensor(t):
-                    t.record_stream(dside)
-            with torch.cuda.stream(dside):
-                loss_d, out, params_full, knn_idx = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
-                                                                        mask_part, target_part_f, src_labels)
-        else:
-            loss_d, out, params_full, knn_idx = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
-                                                                    mask_part, target_part_f, src_labels)
-        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N, share=pp_share).view(B, N, 3)
+        loss_d, out, params_full, knn_idx = self._deform_losses(T, tcode, codes, mats, param_def, x, part_x,
+                                                                mask_part, target_part_f, src_labels)
+        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
         re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
                                                          off=re_in.off).view(B, N, 3)
-        if dside is not None:
-            main.wait_stream(dside)
-            for t in [loss_d, out, params_full] + [v for v in T.values() if torch.is_tensor(v)]:
-                t.record_stream(main)
-            if knn_idx is not None:
-                knn_idx.record_stream(main)
         loss = loss_d
         if cfg["use_residuals_reg"] > 0.0 and epoch > cfg["init_p_m_loss"]:
             # the x -> out NN query of the residual loss is the chamfer full family's second direction
@@ -440,6 +370,14 @@ def batch_to_device(b, device, num_sources=None, bucket=None):
     return out
 
 
+def loader_batching(cfg):
+    """(batch size, shuffle) of the training loader: cfg["batch_size"] and a shuffled order in
+    "train" mode, else 2 and the dataset order (engine/train.py:160-165,174)."""
+    if cfg.get("mode", "train") == "train":
+        return int(cfg["batch_size"]), True
+    return 2, False
+
+
 def make_loader(cfg, db, device, seed=0, dist_src=None):
     if cfg.get("pseudo_labels", True) and dist_src is not None and torch.device(device).type == "cuda":
         return PseudoLabelLoader(cfg, db, device, dist_src, seed=seed)
@@ -475,7 +413,7 @@ class PseudoLabelLoader:
         self.cfg, self.db, self.device, self.seed = cfg, db, device, seed
         P = cfg["MAX_NUM_PARTS"]
         T = int(cfg.get("num_targets", 128))
-        self.bs = cfg["batch_size"]
+        self.bs, self.shuffle = loader_batching(cfg)
         if T < self.bs:
             raise ValueError(f"num_targets ({T}) < batch_size ({self.bs}): every epoch would be empty "
                              "(the reference's DataLoader drops the last partial batch)")
@@ -507,7 +445,8 @@ class PseudoLabelLoader:
     def __iter__(self):
         rng = np.random.Generator(np.random.PCG64([self.seed, self.epoch]))
         self.epoch += 1
-        order = rng.permutation(self.targets["x"].shape[0])
+        T = self.targets["x"].shape[0]
+        order = rng.permutation(T) if self.shuffle else np.arange(T)
         for i in range(self.n):
             sel = order[i * self.bs:(i + 1) * self.bs]
             b = {"x": self.targets["x"][sel], "labels": self.targets["labels"][sel],
@@ -528,7 +467,7 @@ class SyntheticLoader:
 
     def __iter__(self):
         for i in range(self.n):
-            b = synthetic.make_batch(self.cfg["batch_size"], self.cfg.get("num_points", 2048), self.ns,
+            b = synthetic.make_batch(loader_batching(self.cfg)[0], self.cfg.get("num_points", 2048), self.ns,
                                      max_parts=self.cfg["MAX_NUM_PARTS"], parts=self.cfg.get("parts", 4),
                                      seed=self.seed * 100003 + i)
             yield batch_to_device(b, self.device, self.ns, bucket=8 if self.cfg.get("cuda_graph") else None)

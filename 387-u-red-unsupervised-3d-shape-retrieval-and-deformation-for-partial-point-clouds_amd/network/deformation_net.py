@@ -68,16 +68,15 @@ class re_residual_net(nn.Module):
         return [s[0].weight, s[0].bias, s[2].weight, s[2].bias, s[3].weight, s[3].bias, s[5].weight, s[5].bias,
                 s[6].weight, s[6].bias, s[8].weight, s[8].bias, s[9].weight, s[9].bias], [s[2], s[5], s[8]]
 
-    def forward_split(self, pp, code, *, code_first=False, group_rows=0, gidx=None, off=None, rw=None, share=None):
+    def forward_split(self, pp, code, *, code_first=False, group_rows=0, gidx=None, off=None, rw=None):
         """Fused form of forward(cat(pp, code[group(row)])) (or cat(code, pp) if code_first).
 
         pp [M, Cp] point-major, code [G, Cc]; rows grouped by fixed group_rows or by
         gidx (int32 [M]) + off (int32 [G+1], rows of group g = off[g]..off[g+1]).
         rw: optional ured_hip.kernels.RowWeights (unique-row batch, see ResidualNetFn).
-        share: optional ured_hip.ops.SharedGrad slot of pp (its input gradient is summed there).
         """
         params, bns = self._params()
-        spec = (code_first, gidx, off, group_rows, self.training, bns, rw, share)
+        spec = (code_first, gidx, off, group_rows, self.training, bns, rw)
         return ResidualNetFn.apply(spec, pp, code, *params)
 
     def forward(self, concat_feature):

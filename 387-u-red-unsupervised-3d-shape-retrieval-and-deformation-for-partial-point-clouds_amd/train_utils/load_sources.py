@@ -36,14 +36,19 @@ class SourceDB:
         return self.num_sources
 
 
-def connectivity_matrix(arr, n, where="dist_src"):
-    """The [NS, NS] matrix get_labels rows are taken from: a 2-D [n, n] array as is, the cd_m
-    plane of a [3, n, n] sources_connect stack; anything else raises."""
+def connectivity_matrix(arr, n, where="dist_src", plane=2):
+    """The [NS, NS] matrix get_labels rows are taken from: a 2-D [n, n] array as is, plane `plane`
+    (cfg["src_connectivity_plane"], default 2 = cd_m) of a [3, n, n] (dcd, cd_s, cd_m)
+    sources_connect stack; anything else raises. The reference indexes dist_src[label] of
+    whatever array its file holds; no reference file or fixture says which plane that is, so the
+    default is an assumption (the plane PairGenerator writes as M + M.T of cd_m)."""
     arr = np.asarray(arr)
     if arr.shape == (n, n):
         return arr
     if arr.shape == (3, n, n):
-        return arr[2]
+        if plane not in (0, 1, 2):
+            raise ValueError(f"{where}: src_connectivity_plane must be 0 (dcd), 1 (cd_s) or 2 (cd_m), got {plane}")
+        return arr[plane]
     raise ValueError(f"{where}: expected [{n}, {n}] (or a [3, {n}, {n}] dcd/cd_s/cd_m stack), got {arr.shape}")
 
 
@@ -58,9 +63,10 @@ def load_sources(cfg, device=None):
     db = SourceDB(d["src_points"], d["src_mats"], d["src_default_param"], d["src_sem"], device)
     path = cfg.get("src_connectivity")
     if path and os.path.exists(path):
-        dist_src = connectivity_matrix(np.load(path, allow_pickle=False), n, where=path)
+        dist_src = connectivity_matrix(np.load(path, allow_pickle=False), n, where=path,
+                                       plane=int(cfg.get("src_connectivity_plane", 2)))
     elif cfg.get("compute_connectivity", True) and torch.device(device).type == "cuda":
-        dist_src = source_connectivity(db)[2]
+        dist_src = source_connectivity(db)[int(cfg.get("src_connectivity_plane", 2))]
     else:
         dist_src = np.zeros((n, n), np.float64)
     return db, dist_src

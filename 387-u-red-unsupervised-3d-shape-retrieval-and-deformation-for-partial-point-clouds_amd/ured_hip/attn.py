@@ -88,55 +88,6 @@ class CrossAttnFn(Function):
         return dq, dkv, None
 
 
-class SelfAttnPairFn(Function):
-    """Self-attention of two node sets whose fused q|k|v rows are stacked in one [B*n0 + B*n1, 3C]
-    tensor (DescriptorsSelfAttention's two calls, attention_gnn.py:97-118): one ured_attn_fwd /
-    ured_attn_bwd per set on row offsets of the same buffers, so the outputs land in one
-    [rows, C] tensor and the gradient in one [rows, 3C] tensor (no split / cat either way)."""
-
-    @staticmethod
-    def forward(ctx, qkv, B, n0, n1, heads):
-        qkv = qkv.contiguous()
-        R, C3 = qkv.shape
-        C = C3 // 3
-        d = C // heads
-        assert R == B * (n0 + n1)
-        _lib.require_device(qkv)
-        out = torch.empty(R, C, device=qkv.device)
-        ws = []
-        for r0, n in ((0, n0), (B * n0, n1)):
-            w = torch.empty(B, heads, n, n, device=qkv.device)
-            base = qkv.data_ptr() + 4 * r0 * C3
-            _lib.call("ured_attn_fwd", base, C3, base + 4 * C, C3, base + 8 * C, C3, B, heads, n, n, d,
-                      float(d) ** -0.5, out.data_ptr() + 4 * r0 * C, C, w.data_ptr(), _lib.stream_of(out))
-            ws.append(w)
-        ctx.shape = (B, n0, n1, heads)
-        ctx.save_for_backward(qkv, *ws)
-        return out
-
-    @staticmethod
-    def backward(ctx, dout):
-        qkv, w0, w1 = ctx.saved_tensors
-        B, n0, n1, heads = ctx.shape
-        C3 = qkv.shape[1]
-        C = C3 // 3
-        d = C // heads
-        dout = dout.contiguous()
-        dqkv = torch.empty_like(qkv)
-        for r0, n, w in ((0, n0, w0), (B * n0, n1, w1)):
-            q = qkv.data_ptr() + 4 * r0 * C3
-            dq = dqkv.data_ptr() + 4 * r0 * C3
-            _lib.call("ured_attn_bwd", q, C3, q + 4 * C, C3, q + 8 * C, C3, w.data_ptr(), dout.data_ptr() + 4 * r0 * C,
-                      C, B, heads, n, n, d, float(d) ** -0.5, dq, C3, dq + 4 * C, C3, dq + 8 * C, C3,
-                      _lib.stream_of(dout))
-        return dqkv, None, None, None, None
-
-
-def self_attention_pair(qkv, B, n0, n1, heads):
-    """[B*n0 + B*n1, C]: self_attention of rows [0, B*n0) and of rows [B*n0, end) of qkv."""
-    return SelfAttnPairFn.apply(qkv, B, n0, n1, heads)
-
-
 def self_attention(qkv, heads):
     return SelfAttnFn.apply(qkv, heads)
 

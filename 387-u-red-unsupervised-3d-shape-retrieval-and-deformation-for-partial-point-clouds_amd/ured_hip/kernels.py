@@ -63,7 +63,7 @@ _SHAPE_LOG = [] if os.environ.get("URED_GEMM_SHAPES") else None    # diagnostics
 
 # K slice per split of the few-tile store GEMMs (the per-sample fc layers, M = batch): the
 # per-split K-loop is a chain of dependent DMA round trips, so shorter slices = more workgroups
-_SPLITK_KMIN = int(os.environ.get("URED_SPLITK_KMIN", "32"))
+_SPLITK_KMIN = 32
 
 
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro_a=PRO_NONE, pro_b=PRO_NONE,
@@ -216,12 +216,10 @@ def group_colsum(X, N, G, *, off=None, group_rows=0, ldx=None, out=None, rows=No
     return out
 
 
-def colsum(X, out=None, sw=None):
+def colsum(X, out=None):
     """Column sums of a [R][N] tensor (deterministic: fixed split ranges and combine order);
-    into `out` [N] (contiguous) when given. sw: a sidework.SideWork (short-kernel class)."""
+    into `out` [N] (contiguous) when given."""
     R, N = X.shape
-    if sw is not None:
-        return sw.small(lambda: colsum(X, out), X)
     return group_colsum(X, N, 1, group_rows=R, out=None if out is None else out.view(1, N))[0]
 
 
@@ -233,11 +231,8 @@ def splitk_reduce(ws, splits, M, N, out, ldo, accumulate=False, out_off=0, bias=
               int(bool(accumulate)), _p(bias), _lib.stream_of(out))
 
 
-_WGRAD_WGS = int(os.environ.get("URED_WGRAD_WGS", "512"))        # tuning knobs (bench sweeps)
-_WGRAD_MIN_K = int(os.environ.get("URED_WGRAD_MIN_K", "512"))
-_WGRAD_FEW_MIN_K = int(os.environ.get("URED_WGRAD_FEW_MIN_K", "128"))
-_WGRAD_FEW_WGS = int(os.environ.get("URED_WGRAD_FEW_WGS", "512"))
-_WGRAD_FEW_MAX = int(os.environ.get("URED_WGRAD_FEW_MAX", "256"))
+_WGRAD_WGS, _WGRAD_MIN_K = 512, 512                     # swept in round 2 (choose_splits)
+_WGRAD_FEW_WGS, _WGRAD_FEW_MIN_K, _WGRAD_FEW_MAX = 512, 128, 256
 
 
 def choose_splits(Mo, No, K):
@@ -253,39 +248,20 @@ def choose_splits(Mo, No, K):
 
 
 def wgrad(dY, ldd, X, ldx, Cout, Kin, Mrows, out, ldo, *, out_off=0, X_off=0, pro=PRO_NONE, pro_s=None,
-          pro_t=None, accumulate=False, sw=None):
-    """out[cout][kin] (+)= sum_m dY[m][cout] * pro(X[m][kin]) (split-K over the Mrows points).
-    sw: a sidework.SideWork — the split-K GEMM is its "big" class, the reduce and the skinny
-    edge-layer kernels its "small" class."""
+          pro_t=None, accumulate=False):
+    """out[cout][kin] (+)= sum_m dY[m][cout] * pro(X[m][kin]) (split-K over the Mrows points)."""
     if min(Cout, Kin) <= 4 and max(Cout, Kin) <= 256:     # 3-channel edge layers: no MFMA tile
-        def skinny():
-            ws = torch.empty(SKINNY_WS_BLOCKS * Cout * Kin, device=dY.device)
-            _lib.call("ured_wgrad_skinny", _p(dY), int(ldd), _addr(X, X_off), int(ldx), int(Cout), int(Kin),
-                      int(Mrows), int(pro), _p(pro_s), _p(pro_t), _addr(out, out_off), int(ldo),
-                      int(bool(accumulate)), _p(ws), _lib.stream_of(dY))
-        if sw is not None:
-            sw.small(skinny, dY, X)
-        else:
-            skinny()
+        ws = torch.empty(SKINNY_WS_BLOCKS * Cout * Kin, device=dY.device)
+        _lib.call("ured_wgrad_skinny", _p(dY), int(ldd), _addr(X, X_off), int(ldx), int(Cout), int(Kin),
+                  int(Mrows), int(pro), _p(pro_s), _p(pro_t), _addr(out, out_off), int(ldo),
+                  int(bool(accumulate)), _p(ws), _lib.stream_of(dY))
         return
     splits = choose_splits(Cout, Kin, Mrows)
     if splits == 1 and not accumulate:
-        def one():
-            gemm(Cout, Kin, Mrows, dY, ldd, X, ldx, out, ldo, a_kmajor=True, b_kmajor=True, pro_b=pro,
-                 pro_s=pro_s, pro_t=pro_t, epi=EPI_SPLITK, splits=1, B_off=X_off, C_off=out_off)
-        if sw is not None:
-            sw.big(one, dY, X)
-        else:
-            one()
+        gemm(Cout, Kin, Mrows, dY, ldd, X, ldx, out, ldo, a_kmajor=True, b_kmajor=True, pro_b=pro,
+             pro_s=pro_s, pro_t=pro_t, epi=EPI_SPLITK, splits=1, B_off=X_off, C_off=out_off)
         return
-
-    def part():
-        ws = torch.empty(splits, Cout, Kin, device=dY.device)
-        gemm(Cout, Kin, Mrows, dY, ldd, X, ldx, ws, Kin, a_kmajor=True, b_kmajor=True, pro_b=pro,
-             pro_s=pro_s, pro_t=pro_t, epi=EPI_SPLITK, splits=splits, B_off=X_off)
-        return ws
-    if sw is None:
-        splitk_reduce(part(), splits, Cout, Kin, out, ldo, accumulate, out_off)
-        return
-    ws = sw.big(part, dY, X)
-    sw.small(lambda: splitk_reduce(ws, splits, Cout, Kin, out, ldo, accumulate, out_off), ws)
+    ws = torch.empty(splits, Cout, Kin, device=dY.device)
+    gemm(Cout, Kin, Mrows, dY, ldd, X, ldx, ws, Kin, a_kmajor=True, b_kmajor=True, pro_b=pro,
+         pro_s=pro_s, pro_t=pro_t, epi=EPI_SPLITK, splits=splits, B_off=X_off)
+    splitk_reduce(ws, splits, Cout, Kin, out, ldo, accumulate, out_off)

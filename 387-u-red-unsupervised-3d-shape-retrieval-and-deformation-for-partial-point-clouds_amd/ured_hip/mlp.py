@@ -13,19 +13,15 @@ ResidualNetFn  : re_residual_net.forward (network/deformation_net.py:96-107) wit
 Both run forward and backward entirely on HIP kernels; only the tiny
 per-call index bookkeeping is Python.
 """
-import os
-
 import torch
 from torch.autograd import Function
 
 from . import _lib
 from . import kernels as K
-from . import node, syncbn
+from . import node
 from .optim import grad_buffer
-from .sidework import SideWork
 
 BN_EPS = 1e-5
-_BIAS_BATCH = os.environ.get("URED_BIAS_BATCH", "1") != "0"
 
 
 class EncoderSpec:
@@ -148,7 +144,6 @@ class PointEncoderFn(Function):
         W8, fcW = params[28].reshape(params[28].shape[0], -1), params[30]
         C = W8.shape[0]
         grads = [None] * 32
-        sw = _side_work(dev)
         bias = _BiasSums()
         dcode = torch.zeros(G, C, device=dev) if dcode is None else dcode.contiguous()
         dpp = torch.zeros(M, C, device=dev) if dpp is None else dpp.contiguous()
@@ -157,14 +152,14 @@ class PointEncoderFn(Function):
         dpool = torch.empty(G, NP, device=dev)
         K.gemm(G, NP, C, dcode, C, fcW, NP, dpool, NP, b_kmajor=True)
         dfcW, dfcb = grad_buffer(fcW), grad_buffer(params[31])
-        K.wgrad(dcode, C, pooled, NP, C, NP, G, dfcW, NP, sw=sw)
-        K.colsum(dcode, out=dfcb, sw=sw)
+        K.wgrad(dcode, C, pooled, NP, C, NP, G, dfcW, NP)
+        K.colsum(dcode, out=dfcb)
         grads[30], grads[31] = dfcW, dfcb
         # per_point_out.3 (no BN): dW8 = dpp^T @ H7
         dW8, db8 = grad_buffer(params[28]).view(W8.shape), grad_buffer(params[29])
         K.wgrad(dpp, C, Ys[6], Ys[6].shape[1], C, W8.shape[1], M, dW8, W8.shape[1],
-                pro=K.PRO_ENC, pro_s=states[6].scale, pro_t=states[6].shift, sw=sw)
-        K.colsum(dpp, out=db8, sw=sw)
+                pro=K.PRO_ENC, pro_s=states[6].scale, pro_t=states[6].shift)
+        K.colsum(dpp, out=db8)
         grads[28], grads[29] = dW8.view(params[28].shape), db8
         dY, Wn = dpp, W8   # gradient at the output of the layer above, and that layer's weight
         for i in range(6, -1, -1):
@@ -184,14 +179,13 @@ class PointEncoderFn(Function):
             dYi, cs = K.bn_bwd_apply(G_, Y, False, st.mean, coefs, rw=spec.rw)
             W = Ws[i]
             dW, db = grad_buffer(params[4 * i]).view(W.shape), grad_buffer(params[4 * i + 1])
-            _enc_layer_wgrad(sw, spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW)
+            _enc_layer_wgrad(spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW)
             bias.add(cs, db)
             grads[4 * i] = dW.view(params[4 * i].shape)
             grads[4 * i + 1] = db
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
         bias.flush()
-        sw.join()
         return (None, None, None) + tuple(grads)
 
 
@@ -205,9 +199,6 @@ class _BiasSums:
         self.jobs = []
 
     def add(self, cs, out):
-        if not _BIAS_BATCH:                  # A/B knob URED_BIAS_BATCH=0: one column-sum launch per layer
-            K.colsum(cs, out=out)
-            return out
         self.jobs.append((cs, out))
         return out
 
@@ -217,28 +208,21 @@ class _BiasSums:
         self.jobs = []
 
 
-def _side_work(dev):
-    """The weight-gradient side stream of a chain backward (ured_hip/sidework.py); one stream
-    while SyncBN is on (its collectives split a captured graph, which needs no open fork)."""
-    return SideWork(dev, mode=0 if syncbn.active() else None)
-
-
-def _enc_layer_wgrad(sw, spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW):
-    """Weight gradient of TargetEncoder layer i from its dY (side-stream classes)."""
+def _enc_layer_wgrad(spec, i, N, M, G, GR, x, sem, Ys, states, dYi, cs, W, dW):
+    """Weight gradient of TargetEncoder layer i from its dY."""
     if i == 0:
-        K.wgrad(dYi, N, x, 3, N, 3, M, dW, 3, sw=sw)
+        K.wgrad(dYi, N, x, 3, N, 3, M, dW, 3)
     else:
         Xp, stp = Ys[i - 1], states[i - 1]
         kin = Xp.shape[1]
-        K.wgrad(dYi, N, Xp, kin, N, kin, M, dW, W.shape[1], pro=K.PRO_ENC, pro_s=stp.scale, pro_t=stp.shift, sw=sw)
+        K.wgrad(dYi, N, Xp, kin, N, kin, M, dW, W.shape[1], pro=K.PRO_ENC, pro_s=stp.scale, pro_t=stp.shift)
         if i == 5:   # semantic columns of fuse_sem
             S = sem.shape[1]
             if spec.mode == "src":
                 # G-row GEMM on the per-group sums: short work
-                sw.small(lambda: K.wgrad(_group_sums(dYi, cs, N, G, GR), N, sem, S, N, S, G, dW, W.shape[1],
-                                         out_off=kin), dYi, cs, sem)
+                K.wgrad(_group_sums(dYi, cs, N, G, GR), N, sem, S, N, S, G, dW, W.shape[1], out_off=kin)
             else:
-                K.wgrad(dYi, N, sem, S, N, S, M, dW, W.shape[1], out_off=kin, sw=sw)
+                K.wgrad(dYi, N, sem, S, N, S, M, dW, W.shape[1], out_off=kin)
 
 
 def _group_sums(dY, cs, N, G, group_rows):
@@ -306,15 +290,12 @@ class ResidualNetFn(Function):
         K.gemm(M, W4.shape[0], kin, h, kin, W4, W4.shape[1], out, W4.shape[0], pro_a=K.PRO_RES,
                pro_s=st.scale, pro_t=st.shift, bias=params[13])
         ctx.spec, ctx.states = spec, states
-        if len(spec) > 7 and spec[7] is not None:
-            spec[7].register()              # ops.SharedGrad slot of pp
         ctx.save_for_backward(pp, code, *Ys, *params)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         code_first, gidx, off, group_rows, training, bn_modules, rw = ctx.spec[:7]
-        share = ctx.spec[7] if len(ctx.spec) > 7 else None     # ops.SharedGrad slot of pp
         states = ctx.states
         saved = ctx.saved_tensors
         pp, code = saved[:2]
@@ -324,15 +305,14 @@ class ResidualNetFn(Function):
         G, Cc = code.shape
         dev = pp.device
         grads = [None] * 14
-        sw = _side_work(dev)
         bias = _BiasSums()
         dout = dout.contiguous()
         W4 = params[12].reshape(params[12].shape[0], -1)
         No = W4.shape[0]
         dW4, db4 = grad_buffer(params[12]).view(W4.shape), grad_buffer(params[13])
         K.wgrad(dout, No, Ys[2], Ys[2].shape[1], No, W4.shape[1], M, dW4, W4.shape[1],
-                pro=K.PRO_RES, pro_s=states[2].scale, pro_t=states[2].shift, sw=sw)
-        K.colsum(dout, out=db4, sw=sw)
+                pro=K.PRO_RES, pro_s=states[2].scale, pro_t=states[2].shift)
+        K.colsum(dout, out=db4)
         grads[12], grads[13] = dW4.view(params[12].shape), db4
         dY, Wn = dout, W4
         W1 = params[0].reshape(params[0].shape[0], -1)
@@ -353,38 +333,28 @@ class ResidualNetFn(Function):
             W = params[4 * i].reshape(params[4 * i].shape[0], -1)
             dW, db = grad_buffer(params[4 * i]).view(W.shape), grad_buffer(params[4 * i + 1])
             if i == 0:
-                K.wgrad(dYi, N, pp, Cp, N, Cp, M, dW, ld1, out_off=pp_off, sw=sw)
-
-                def first(N=N, dYi=dYi, cs=cs, dW=dW, db=db):    # G-row work: short kernels
-                    if Cc > 0:
-                        if off is not None:
-                            D = K.group_colsum(dYi, N, G, off=off)
-                        else:
-                            D = _group_sums(dYi, cs, N, G, group_rows)
-                        K.wgrad(D, N, code, Cc, N, Cc, G, dW, ld1, out_off=code_off)
-                        # dcode = D @ W1[:, code cols]
-                        K.gemm(G, Cc, N, D, N, W1, ld1, dcode, Cc, b_kmajor=True, B_off=code_off)
-                sw.small(first, dYi, cs, dcode, code)
+                K.wgrad(dYi, N, pp, Cp, N, Cp, M, dW, ld1, out_off=pp_off)
+                if Cc > 0:                     # G-row work on the per-group sums: short kernels
+                    if off is not None:
+                        D = K.group_colsum(dYi, N, G, off=off)
+                    else:
+                        D = _group_sums(dYi, cs, N, G, group_rows)
+                    K.wgrad(D, N, code, Cc, N, Cc, G, dW, ld1, out_off=code_off)
+                    # dcode = D @ W1[:, code cols]
+                    K.gemm(G, Cc, N, D, N, W1, ld1, dcode, Cc, b_kmajor=True, B_off=code_off)
             else:
                 Xp, stp = Ys[i - 1], states[i - 1]
                 K.wgrad(dYi, N, Xp, Xp.shape[1], N, Xp.shape[1], M, dW, W.shape[1],
-                        pro=K.PRO_RES, pro_s=stp.scale, pro_t=stp.shift, sw=sw)
+                        pro=K.PRO_RES, pro_s=stp.scale, pro_t=stp.shift)
             bias.add(cs, db)
             grads[4 * i] = dW.view(params[4 * i].shape)
             grads[4 * i + 1] = db
             grads[4 * i + 2], grads[4 * i + 3] = dgamma, dbeta
             dY, Wn = dYi, W
         bias.flush()
-        # input gradient dpp = dY1 @ W1[:, pp cols] (dcode on the side stream, above)
+        # input gradient dpp = dY1 @ W1[:, pp cols]
         dpp = torch.empty(M, Cp, device=dev)
         K.gemm(M, Cp, W1.shape[0], dY, W1.shape[0], W1, ld1, dpp, Cp, b_kmajor=True, B_off=pp_off)
-        sw.join()
-        if share is not None:        # pp's other consumer sums into this buffer (or already did)
-            if share.buf is None:
-                share.buf = dpp
-            else:
-                share.buf.view(M, Cp).add_(dpp)
-            dpp = share.finish((M, Cp))
         return (None, dpp, dcode) + tuple(grads)
 
 

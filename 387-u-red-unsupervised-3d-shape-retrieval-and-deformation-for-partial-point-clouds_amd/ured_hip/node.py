@@ -268,20 +268,6 @@ def _w2(conv):
     return conv.weight.view(conv.weight.shape[0], -1)
 
 
-def _share_target(share, x):
-    """(buffer, accumulate) for the input gradient of x: a fresh tensor without a SharedGrad
-    slot; with one, the slot's buffer (accumulate) or a fresh tensor that becomes it."""
-    if share is None:
-        return torch.empty(x.shape, device=x.device), False
-    if share.buf is not None:
-        buf = share.buf.view(x.shape)
-        if not buf.is_contiguous():
-            raise ValueError("shared gradient buffer must be contiguous")
-        return buf, True
-    share.buf = torch.empty(x.shape, device=x.device)
-    return share.buf, False
-
-
 class NodeLinearFn(Function):
     """y = x W^T + b (+ R). x [M, K] (any row stride, unit column stride), W [N, K]."""
 
@@ -381,13 +367,9 @@ class NodeProjFn(Function):
     apply(groups, x_0, .., x_{n-1}, then per input: its weights, then its biases)."""
 
     @staticmethod
-    def forward(ctx, groups, shares, *tensors):
+    def forward(ctx, groups, *tensors):
         n = len(groups)
         xs, rest = tensors[:n], tensors[n:]
-        ctx.shares = shares
-        for sh in shares:
-            if sh is not None:
-                sh.register()
         _lib.require_device(*xs)
         Ws, bs, o = [], [], 0
         for gsz in groups:
@@ -417,28 +399,27 @@ class NodeProjFn(Function):
             o += 2 * gsz
             g = _rows(gs[i])
             x = xs[i]
-            dx, adx = _share_target(ctx.shares[i], x)
+            dx = torch.empty(x.shape, device=x.device)
             dW, aW, fW = _grad_rows(w)
             db, ab, fb = _grad_rows(b)
-            jobs += [dgrad_desc(g, _stack_rows(w), dx, accumulate=adx), wgrad_desc(g, x, dW, accumulate=aW),
+            jobs += [dgrad_desc(g, _stack_rows(w), dx), wgrad_desc(g, x, dW, accumulate=aW),
                      colsum_desc(g, db, accumulate=ab)]
             dxs.append(dx)
             fins.append((fW, fb))
         launch(*jobs)
-        dxs = [dx if sh is None else sh.finish(dx.shape) for dx, sh in zip(dxs, ctx.shares)]
-        out = [None, None] + dxs
+        out = [None] + dxs
         for fW, fb in fins:
             out += fW() + fb()
         return tuple(out)
 
 
-def node_proj(xs, groups_w, groups_b, shares=None):
+def node_proj(xs, groups_w, groups_b):
     """NodeProjFn over inputs xs with weight groups groups_w[i] (tuples of [N_j, K] tensors) and
-    bias groups groups_b[i]; shares[i]: a SharedGrad slot of xs[i] (ured_hip/ops.py) or None."""
+    bias groups groups_b[i]."""
     args = list(xs)
     for w, b in zip(groups_w, groups_b):
         args += list(w) + list(b)
-    return NodeProjFn.apply(tuple(len(w) for w in groups_w), tuple(shares or (None,) * len(xs)), *args)
+    return NodeProjFn.apply(tuple(len(w) for w in groups_w), *args)
 
 
 class NodeFFNFn(Function):
@@ -451,8 +432,6 @@ class NodeFFNFn(Function):
     @staticmethod
     def forward(ctx, spec, x, msg, R, W1, b1, gamma, beta, W2, b2):
         bnm, off, training = spec[:3]
-        if len(spec) > 3 and spec[3] is not None:
-            spec[3].register()
         ctx.res_is_x = R is None
         R = x if R is None else R
         M, C = x.shape
@@ -473,7 +452,6 @@ class NodeFFNFn(Function):
     @staticmethod
     def backward(ctx, g):
         bnm, off, training = ctx.spec[:3]
-        share = ctx.spec[3] if len(ctx.spec) > 3 else None     # SharedGrad slot of x
         x, msg, W1, gamma, W2, Y1, act, mean, invstd, b1, beta, b2 = ctx.saved_tensors
         g = _rows(g)
         M, C = x.shape
@@ -491,28 +469,20 @@ class NodeFFNFn(Function):
                 (buf.add_ if acc else buf.copy_)(tmp)
         (dW1, aW1), (db1, ab1) = grad_slot(W1), grad_slot(b1)
         R = g if ctx.res_is_x else None
-        if share is None:
-            dxm = torch.empty(M, 2 * C, device=dev)           # [d first | d message] in one GEMM
-            launch(wgrad_desc(dY1, x, dW1, accumulate=aW1, x2=msg),
-                   dgrad_desc(dY1, W1, dxm, R=R, R_ncols=C), colsum_desc(dY1, db1, accumulate=ab1))
-            dx, dmsg = dxm[:, :C], dxm[:, C:]
-        else:                  # d first summed into the shared buffer of x by the GEMM itself
-            dxs, adx = _share_target(share, x)
-            dmsg = torch.empty(M, C, device=dev)
-            launch(wgrad_desc(dY1, x, dW1, accumulate=aW1, x2=msg),
-                   dgrad_desc(dY1, W1[:, :C], dxs, R=R, R_ncols=C, accumulate=adx),
-                   dgrad_desc(dY1, W1[:, C:], dmsg), colsum_desc(dY1, db1, accumulate=ab1))
-            dx = share.finish(x.shape)
+        dxm = torch.empty(M, 2 * C, device=dev)               # [d first | d message] in one GEMM
+        launch(wgrad_desc(dY1, x, dW1, accumulate=aW1, x2=msg),
+               dgrad_desc(dY1, W1, dxm, R=R, R_ncols=C), colsum_desc(dY1, db1, accumulate=ab1))
+        dx, dmsg = dxm[:, :C], dxm[:, C:]
         return (None, dx, dmsg, (None if ctx.res_is_x else g),
                 *(None if acc else t for t, acc in ((dW1, aW1), (db1, ab1), (dgamma, ag), (dbeta, abe), (dW2, aW2),
                                                     (db2, ab2))))
 
 
-def node_ffn(fc, x, msg, R, off, share=None):
+def node_ffn(fc, x, msg, R, off):
     """FeedForwardNet_norm([2C, 2C, C], use_bn) `fc` on cat([x, msg]) + R (None: + x), node
-    sets `off`; share: a SharedGrad slot of x (ured_hip/ops.py) or None."""
+    sets `off`."""
     conv1, bnm, conv2 = fc[0], fc[2], fc[3]
-    spec = (bnm, tuple(int(o) for o in off), bnm.training, share)
+    spec = (bnm, tuple(int(o) for o in off), bnm.training)
     return NodeFFNFn.apply(spec, x, msg, R, _w2(conv1), conv1.bias, bnm.weight, bnm.bias, _w2(conv2), conv2.bias)
 
 

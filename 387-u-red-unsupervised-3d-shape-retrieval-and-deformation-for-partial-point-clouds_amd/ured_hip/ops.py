@@ -9,7 +9,6 @@ PartBatch     : the ragged per-part view of a target batch that the reference
 build_parts   : computes a PartBatch with device ops only (no host sync).
 """
 import ctypes
-import os
 
 import torch
 from torch.autograd import Function
@@ -78,68 +77,6 @@ def permute_rows(x, perm, inv):
     return PermuteRowsFn.apply(x, perm, inv)
 
 
-class SharedGrad:
-    """The gradient of a tensor that several HIP Functions consume, summed by their kernels
-    instead of by autograd. share_grad(x) returns (x', slot); each consumer built with the slot
-    returns no gradient for x' and, in its backward, writes its gradient into slot.buf (the first
-    one to run) or accumulates into it (a later one: in its own kernel where it can, else one
-    add); ShareFn's backward — which autograd runs after every consumer of x' — hands slot.buf
-    on as x's gradient (plus any gradient x' received from ordinary consumers). Used for the
-    target per-point features pp, read by get_part's regrouping and the reconstruction decoder
-    (engine/train.py:240,250): one [B*N, C] pass less per step."""
-    __slots__ = ("buf", "expected", "done")
-
-    def __init__(self):
-        self.buf, self.expected, self.done = None, 0, 0
-
-    def register(self):
-        """A consumer's forward: one more backward will write into this slot."""
-        self.expected += 1
-
-    def finish(self, shape):
-        """A consumer's backward, after writing: the finished sum (viewed as `shape`) for the last
-        registered consumer to hand autograd as its input gradient — so ShareFn's node receives a
-        defined gradient and runs on the device queue — else None."""
-        self.done += 1
-        if self.done < self.expected or self.buf is None:
-            return None
-        b, self.buf = self.buf, None
-        return b.view(shape)
-
-
-class ShareFn(Function):
-    @staticmethod
-    def forward(ctx, x, slot):
-        ctx.slot, ctx.shape = slot, x.shape
-        ctx.set_materialize_grads(False)
-        return x.view_as(x)
-
-    @staticmethod
-    def backward(ctx, g):
-        buf, ctx.slot.buf = ctx.slot.buf, None
-        if buf is None:
-            return g, None
-        buf = buf.view(ctx.shape)
-        return (buf if g is None else buf + g), None
-
-
-# Opt-in (URED_SHARE_GRAD=1): +0.5 % on the config-2 step, bitwise-tested, but the 8-rank
-# data-parallel test (tests/test_dp_configs_gpu.py config 5: eight processes on one GPU, gloo,
-# bucketed all-reduce from backward hooks) hit a GPU memory fault 2 of 2 times with it (and
-# URED_ATTN_PAIR) on, 0 of 2 with both off, and passed with kernels serialised
-# (AMD_SERIALIZE_KERNEL=3): an ordering hazard not yet found, so it stays off by default.
-SHARE_GRAD = os.environ.get("URED_SHARE_GRAD", "0") == "1"
-
-
-def share_grad(x):
-    """(x', SharedGrad) — see SharedGrad; (x, None) unless URED_SHARE_GRAD=1 (see SHARE_GRAD)."""
-    if not SHARE_GRAD:
-        return x, None
-    slot = SharedGrad()
-    y = ShareFn.apply(x, slot)
-    return y, slot
-
-
 class PartRowsFn(Function):
     """get_part's regrouping of per-point features (engine/train.py:103-136): x [B, N, C] ->
     (rows sorted by part label [B*N, C], per-part-slot sums [G, C]). Forward: one gather and one
@@ -147,7 +84,7 @@ class PartRowsFn(Function):
     take an index_select of the part gradients, an add and the inverse-permutation gather."""
 
     @staticmethod
-    def forward(ctx, x, perm, inv, off, gid, share=None):
+    def forward(ctx, x, perm, inv, off, gid):
         B, N, C = x.shape
         x = x.contiguous()
         if perm.dtype != torch.int64 or gid.dtype != torch.int32:
@@ -161,9 +98,6 @@ class PartRowsFn(Function):
         sums = K.group_colsum(xs, C, off.shape[0] - 1, off=off)
         ctx.save_for_backward(inv, gid)
         ctx.shape = (B, N, C)
-        ctx.share = share
-        if share is not None:
-            share.register()
         return xs, sums
 
     @staticmethod
@@ -174,24 +108,16 @@ class PartRowsFn(Function):
         dg = None if d_sums is None else d_sums.contiguous()
         if inv.dtype != torch.int64 or gid.dtype != torch.int32:
             raise TypeError("part_rows: inv must be int64 and gid int32")
-        sh = ctx.share
-        acc = None if sh is None else sh.buf        # another consumer's gradient of x: add in the kernel
-        out = torch.empty(B, N, C, device=inv.device) if acc is None else acc
-        if acc is not None and (not acc.is_contiguous() or acc.numel() != B * N * C):
-            raise ValueError("part_rows: shared gradient buffer must be a contiguous [B*N, C] tensor")
-        _lib.call("ured_part_rows_bwd_add", _lib.ptr(ds), _lib.ptr(dg), _lib.ptr(inv.contiguous()),
-                  _lib.ptr(gid.contiguous()), B, N, C, _lib.ptr(acc), _lib.ptr(out), _lib.stream_of(out))
-        if sh is not None:
-            sh.buf = out
-            return sh.finish((B, N, C)), None, None, None, None, None
-        return out, None, None, None, None, None
+        out = torch.empty(B, N, C, device=inv.device)
+        _lib.call("ured_part_rows_bwd", _lib.ptr(ds), _lib.ptr(dg), _lib.ptr(inv.contiguous()),
+                  _lib.ptr(gid.contiguous()), B, N, C, _lib.ptr(out), _lib.stream_of(out))
+        return out, None, None, None, None
 
 
-def part_rows(x, parts, share=None):
-    """(x regrouped by part [B*N, C], per-part-slot sums [B*P, C]) for a PartBatch; `share`: a
-    SharedGrad slot of x (its gradient is then summed there, see SharedGrad)."""
+def part_rows(x, parts):
+    """(x regrouped by part [B*N, C], per-part-slot sums [B*P, C]) for a PartBatch."""
     _lib.require_device(x)
-    return PartRowsFn.apply(x, parts.perm, parts.inv_perm, parts.off, parts.gid, share)
+    return PartRowsFn.apply(x, parts.perm, parts.inv_perm, parts.off, parts.gid)
 
 
 def segment_sum(x, off, gid):
@@ -326,7 +252,8 @@ def upload(a, device):
 class PartBounds:
     """Host-side bounds of a target batch's part structure, from the host labels (no device sync):
     k = the most parts of any target (rounded up to a multiple of 4) and count = the most points of
-    any one part (rounded up to a multiple of 256). The loss head sizes its chamfer NN launches by
+    any one part (rounded up to a power of two, at least 256: at most 4 x log2 distinct keys, so
+    real part-size distributions do not keep evicting captured graphs). The loss head sizes its chamfer NN launches by
     them instead of by the slot bounds (P x 1024 deformed points, N target points per part): with
     the step's 4 parts per target the full family is 4096 x 2048 per target instead of 16384 x
     2048, small enough for the two-pass kernel's whole-set tile. Part of the HIP-graph key
@@ -341,7 +268,9 @@ class PartBounds:
             _, c = np.unique(row, return_counts=True)
             k, cnt = max(k, int(c.shape[0])), max(cnt, int(c.max()) if c.size else 0)
         self.k = -(-k // 4) * 4
-        self.count = -(-cnt // 256) * 256
+        self.count = 256
+        while self.count < cnt:
+            self.count *= 2
 
     def key(self):
         return (self.k, self.count)

@@ -529,12 +529,8 @@ def main():
     ap.add_argument("--graph-dp", action="store_true", help=argparse.SUPPRESS)   # graph replay is the N > 1 default
     ap.add_argument("--graph-bucket", type=int, default=1,
                     help="graph mode: pad the distinct-source-part count to a multiple of this (one graph per count)")
-    ap.add_argument("--overlap", action="store_true",
-                    help="run the source branch on a second stream (measured neutral: the GEMMs fill the GPU)")
     ap.add_argument("--all-slots", action="store_true",
                     help="encode every source slot (no unique-source encoding) in the timed run")
-    ap.add_argument("--deform-overlap", action="store_true",
-                    help="DeformNet + chamfer/contrast losses on a side stream (overlaps the residual nets)")
     ap.add_argument("--blas", choices=["default", "hipblaslt", "rocblas"], default="rocblas",
                     help="torch matmul backend for the small DeformNet / contrast GEMMs")
     ap.add_argument("--no-extras", action="store_true",
@@ -584,8 +580,6 @@ def main():
     cfg = workload_cfg(args)
     use_graph = not args.eager
     cfg["cuda_graph"] = use_graph
-    cfg["stream_overlap"] = args.overlap
-    cfg["deform_overlap"] = args.deform_overlap
     db, _ = load_sources(cfg, dev)
     eager = DataParallelStep(cfg, db, dev)
     cfg["unique_sources"] = not args.all_slots

@@ -66,28 +66,6 @@ def test_self_attention_matches_reference(dev, B, H, n, d):
     _close(x.grad, xr.grad)
 
 
-@pytest.mark.parametrize("B,H,n0,n1,d", [(16, 4, 16, 2, 128), (3, 2, 5, 7, 16)])
-def test_self_attention_pair_equals_two_calls(dev, B, H, n0, n1, d):
-    """SelfAttnPairFn (both node sets of a DescriptorsSelfAttention layer on row offsets of one
-    q|k|v buffer) == self_attention of each set separately: output and q|k|v gradient bitwise."""
-    from ured_hip.attn import self_attention, self_attention_pair
-    g = torch.Generator().manual_seed(n0 * 7 + n1)
-    C = H * d
-    R0, R1 = B * n0, B * n1
-    qkv = torch.randn(R0 + R1, 3 * C, generator=g).to(dev)
-    go = torch.randn(R0 + R1, C, generator=g).to(dev)
-    a = qkv.clone().requires_grad_(True)
-    out = self_attention_pair(a, B, n0, n1, H)
-    out.backward(go)
-    b = qkv.clone().requires_grad_(True)
-    q0, q1 = b.split([R0, R1])
-    ref = torch.cat([self_attention(q0.view(B, n0, -1), H).reshape(R0, C),
-                     self_attention(q1.view(B, n1, -1), H).reshape(R1, C)])
-    ref.backward(go)
-    assert torch.equal(out, ref)
-    assert torch.equal(a.grad, b.grad)
-
-
 def test_attention_rejects_oversize(dev):
     from ured_hip import _lib
     from ured_hip.attn import cross_attention

@@ -100,3 +100,38 @@ def test_chain_laid_out_back_to_back(order):
     fused = fused_rows(ws)
     assert fused is not None and fused.shape == (48, 16)
     assert torch.equal(fused, torch.cat([w.detach() for w in ws]))
+
+
+def test_post_accumulate_hook_sees_the_complete_sum_once():
+    """The ownership argument of the in-kernel accumulation ("Gradient buffers"): the
+    parameter's AccumulateGrad node has one input edge per use, so it runs ONCE, after every
+    use's backward has run; the first claim handed it a defined tensor (the flat view), so it is
+    scheduled on the device queue like any other node. The post-accumulate hook that issues a
+    data-parallel bucket's all-reduce (engine/dp.py) therefore fires once per backward, on the
+    flat view itself, with both uses' contributions already in it."""
+    W, V, opt, x = _setup()
+    x2 = torch.randn(4, 3)
+    seen = []
+    W.register_post_accumulate_grad_hook(lambda p: seen.append((p.grad.data_ptr(), p.grad.clone())))
+    opt.zero_grad(set_to_none=True)
+    y = _Lin.apply(x, W)
+    (_Lin.apply(x2, W).sum() + y.sum()).backward()
+    assert len(seen) == 1
+    ptr, val = seen[0]
+    assert ptr == _view(opt, W).data_ptr()
+    torch.testing.assert_close(val, torch.ones(4, 5).t() @ x + torch.ones(4, 5).t() @ x2)
+
+
+def test_accumulated_view_replaced_by_autograd_raises():
+    """Guard of the accumulate contract: a non-HIP producer of the same parameter's gradient
+    between two HIP uses makes autograd sum out of place, so a later in-kernel add lands in a
+    tensor autograd no longer holds; gather_grads() raises instead of losing it."""
+    W, V, opt, x = _setup()
+    x2, x3 = torch.randn(4, 3), torch.randn(4, 3)
+    opt.zero_grad(set_to_none=True)
+    a = _Lin.apply(x, W)            # backward runs last: claims the view with accumulate=True
+    b = x2 @ W.t()                  # an ordinary op: a fresh gradient tensor
+    c = _Lin.apply(x3, W)           # backward runs first: claims the view
+    (a.sum() + b.sum() + c.sum()).backward()
+    with pytest.raises(RuntimeError, match="replaced by autograd"):
+        opt.gather_grads()

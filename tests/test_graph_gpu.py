@@ -118,58 +118,28 @@ def test_graph_replay_across_residual_gate(dev):
             assert torch.equal(pa, pb), (name, k)
 
 
-def test_wgrad_side_stream_equals_one_stream(dev, monkeypatch):
-    """The weight-gradient side stream (ured_hip/sidework.py) changes only where the wgrad /
-    reduce / bias-sum kernels run, not what they compute: eager steps with either side-stream
-    mode and graph-replayed steps (mode 2) equal one-stream eager steps bitwise."""
+@pytest.mark.parametrize("opt", ["adam", "sgd"])
+def test_graph_replay_follows_scheduler_with_torch_optimizers(dev, opt):
+    """torch's Adam / SGD (cfg flat_adam: false, or optimizer sgd) bake the float learning rate
+    into the captured update graph: GraphedStep re-captures that graph when StepLR changes the
+    lr, so replayed steps across a scheduler step equal eager steps bitwise (FlatAdam reads its
+    lr from a device scalar instead)."""
     from dataset import synthetic
     from engine.graph import GraphedStep
     from engine.train import batch_to_device
-    from ured_hip import sidework
-    cfg = dict(CFG, cuda_graph=True)
-    batches = [batch_to_device(synthetic.make_batch(2, 128, 24, parts=[3, 2], seed=80 + i), dev) for i in range(3)]
-    steps = {m: _make(dev, cfg) for m in (0, 1, 2)}
-    monkeypatch.setattr(sidework, "MODE", 2)
-    gs = _make(dev, cfg)
-    g = GraphedStep(gs, batches[0], warmup=2)         # 2 eager steps on batch 0, then capture
-    for _ in range(2):
-        for m, st in steps.items():
-            monkeypatch.setattr(sidework, "MODE", m)
-            st.step(batches[0])
-    for rnd in range(2):
-        for i, bt in enumerate(batches):
-            monkeypatch.setattr(sidework, "MODE", 2)
-            lg = g.step(bt)["all_loss"].clone()
-            ls = {}
-            for m, st in steps.items():
-                monkeypatch.setattr(sidework, "MODE", m)
-                ls[m] = st.step(bt)["all_loss"]
-            assert all(torch.equal(v, ls[0]) for v in ls.values()), (rnd, i, {m: v.item() for m, v in ls.items()})
-            assert torch.equal(lg, ls[0]), (rnd, i, lg.item(), ls[0].item())
-    for name in gs.models:
-        ref = list(steps[0].models[name].state_dict().items())
-        for other in (steps[1], steps[2], gs):
-            for (k, pa), (_, pb) in zip(ref, other.models[name].state_dict().items()):
-                assert torch.equal(pa, pb), (name, k)
-
-
-def test_shared_gradients_match_autograd_sums(dev, monkeypatch):
-    """The opt-in in-kernel gradient sums (ured_hip/ops.py SharedGrad, URED_SHARE_GRAD=1, with the
-    self-attention node-set pair) against the default autograd sums: three eager steps agree in
-    their losses to 1e-5 relative (the sums of three or more gradients associate differently, and
-    Adam turns rounding-level gradient differences of near-zero entries into visible parameter
-    differences, so the parameters themselves are not compared)."""
-    import attention_graph.attention_gnn as agn
-    from dataset import synthetic
-    from engine.train import batch_to_device
-    from ured_hip import ops
-    batches = [batch_to_device(synthetic.make_batch(2, 128, 24, parts=[3, 2], seed=110 + i), dev) for i in range(3)]
-    a, b = _make(dev, CFG), _make(dev, CFG)
-    for bt in batches:
-        monkeypatch.setattr(ops, "SHARE_GRAD", True)
-        monkeypatch.setattr(agn, "_ATTN_PAIR", True)
-        la = a.step(bt)["all_loss"].item()
-        monkeypatch.setattr(ops, "SHARE_GRAD", False)
-        monkeypatch.setattr(agn, "_ATTN_PAIR", False)
-        lb = b.step(bt)["all_loss"].item()
-        assert abs(la - lb) <= 1e-5 * abs(lb), (la, lb)
+    cfg = dict(CFG, cuda_graph=True, flat_adam=False, optimizer=opt, momentum=0.9, lr_stepsize=1, lr_decay=0.5)
+    batches = [batch_to_device(synthetic.make_batch(2, 128, 24, parts=[3, 2], seed=90 + i), dev) for i in range(3)]
+    a, b = _make(dev, cfg), _make(dev, cfg)
+    assert not hasattr(a.optimizer, "sync_lr")
+    g = GraphedStep(a)
+    for ep in range(3):
+        for bt in batches:
+            la = g.step(bt)["all_loss"].clone()
+            lb = b.step(bt)["all_loss"]
+            assert torch.equal(la, lb), (ep, la.item(), lb.item())
+        g.scheduler.step()
+        b.scheduler.step()
+    assert g.update_captures >= 3                      # one per learning rate
+    for name in a.models:
+        for (k, pa), (_, pb) in zip(a.models[name].state_dict().items(), b.models[name].state_dict().items()):
+            assert torch.equal(pa, pb), (name, k)

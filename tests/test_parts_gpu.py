@@ -90,54 +90,6 @@ def test_part_rows_matches_separate_ops(dev, B, N, P, C, kmax):
         assert torch.equal(a.grad, b.grad), (a.grad - b.grad).abs().max().item()
 
 
-@pytest.mark.parametrize("C", [512, 6])
-def test_part_rows_shared_gradient(dev, C, monkeypatch):
-    """pp read by get_part's regrouping and by another consumer (the reconstruction decoder),
-    its two gradients summed by the kernels through a SharedGrad slot (ured_part_rows_bwd_add,
-    in place) == autograd's sum of the two, bitwise, whichever consumer's backward runs first;
-    a gradient the shared tensor also receives from an ordinary op is added too."""
-    from ured_hip import ops
-    from ured_hip.ops import build_parts, part_rows, share_grad
-    monkeypatch.setattr(ops, "SHARE_GRAD", True)      # opt-in in the product (ops.SHARE_GRAD)
-    B, N, P = 4, 300, 16
-    g = torch.Generator().manual_seed(C)
-    x = torch.randn(B, N, C, generator=g).to(dev)
-    parts = build_parts(torch.randint(0, 5, (B, N), generator=g).to(dev), torch.randn(B, N, 3, generator=g).to(dev), P)
-    gs, gp = torch.randn(B * N, C, generator=g).to(dev), torch.randn(B * P, C, generator=g).to(dev)
-    w = torch.randn(B, N, C, generator=g).to(dev)
-
-    class Other(torch.autograd.Function):       # a consumer that writes / accumulates into the slot
-        @staticmethod
-        def forward(ctx, t, slot):
-            ctx.slot = slot
-            return (t * 1.0).sum()
-
-        @staticmethod
-        def backward(ctx, go):
-            d = w * go
-            if ctx.slot.buf is None:
-                ctx.slot.buf = d
-            else:
-                ctx.slot.buf.view(d.shape).add_(d)
-            return None, None
-
-    b = x.clone().requires_grad_(True)
-    xs, sums = part_rows(b, parts)
-    torch.autograd.backward([xs, sums, (b * w).sum(), (b * 2.0).sum()], [gs, gp, None, None])
-    for other_first in (False, True):
-        a = x.clone().requires_grad_(True)
-        y, slot = share_grad(a)
-        if other_first:             # created last: its backward runs first
-            xs, sums = part_rows(y, parts, slot)
-            o = Other.apply(y, slot)
-        else:
-            o = Other.apply(y, slot)
-            xs, sums = part_rows(y, parts, slot)
-        torch.autograd.backward([xs, sums, o, (y * 2.0).sum()], [gs, gp, None, None])
-        assert slot.buf is None
-        torch.testing.assert_close(a.grad, b.grad, rtol=0, atol=1e-5 * b.grad.abs().max().item())
-
-
 @pytest.mark.parametrize("B,N,P,gaps", [(3, 257, 16, True), (16, 2048, 16, False), (2, 5000, 32, True), (1, 7, 16, True)])
 def test_build_parts_kernel_equals_composed(dev, B, N, P, gaps):
     """ured_build_parts (one launch: stable counting sort, slot tables, boxes, param_def) == the
