@@ -95,3 +95,36 @@ def make_batch(batch_size, num_points, num_sources, max_parts=16, parts=4, seed=
     src_index = np.where(src_labels < 0, num_sources - 1, src_labels)
     return {"x": x, "labels": labels, "tgt_sem": tgt_sem, "src_labels": src_labels,
             "src_index": src_index, "parts": np.asarray(ks, np.int64)}
+
+
+def make_targets_from_sources(src_points, src_sem, num_targets, num_points, parts=4, seed=0):
+    """Targets assembled from source parts (the PartNet situation the pseudo-labels assume: a
+    target part resembles some source part): target j takes k_j distinct random sources, part i
+    is num_points / k_j points drawn (with replacement) from source s_i's cloud at its own place,
+    with that source's semantics; the cloud is shuffled and normalize_pts'ed. The nearest source of
+    each part by calc_dcd is then its own source, so a batch encodes as many distinct source parts
+    as make_batch's uniformly drawn labels do. Returns make_batch's fields plus "src_true"."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    src_points = np.asarray(src_points, np.float32)
+    src_sem = np.asarray(src_sem, np.int64)
+    NS, NPP = src_points.shape[:2]
+    T, N = num_targets, num_points
+    ks = [parts] * T if np.isscalar(parts) else list(parts)
+    x = np.zeros((T, N, 3), np.float32)
+    labels = np.zeros((T, N), np.int64)
+    tgt_sem = np.zeros((T, N), np.int64)
+    src_true = np.full((T, max(ks)), -1, np.int64)
+    for j in range(T):
+        k = ks[j]
+        srcs = rng.choice(NS, size=k, replace=False)
+        sizes = np.full(k, N // k)
+        sizes[:N % k] += 1
+        lab = np.repeat(np.arange(k), sizes)
+        pts = np.concatenate([src_points[s][rng.integers(0, NPP, size=n)] for s, n in zip(srcs, sizes)])
+        order = rng.permutation(N)
+        x[j] = normalize_pts(pts[order])
+        labels[j] = lab[order]
+        tgt_sem[j] = src_sem[srcs][labels[j]]
+        src_true[j, :k] = srcs
+    return {"x": x, "labels": labels, "tgt_sem": tgt_sem, "parts": np.asarray(ks, np.int64), "src_true": src_true}
+

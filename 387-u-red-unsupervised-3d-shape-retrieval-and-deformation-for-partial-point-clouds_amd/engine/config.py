@@ -40,7 +40,7 @@ REFERENCE_UNREAD = {
 EXTRA = {
     "synthetic", "seed", "num_points", "parts", "num_targets", "iters_per_epoch", "pseudo_labels",
     "unique_sources", "flat_adam", "fused_adam", "cuda_graph",
-    "log_every", "compute_connectivity", "src_connectivity_plane", "differentiable_gather", "sync_bn", "loss_head", "dist_backend",
+    "log_every", "compute_connectivity", "src_connectivity_plane", "synthetic_targets", "differentiable_gather", "sync_bn", "loss_head", "dist_backend",
 }
 
 TRAIN_REQUIRED = ("source_latent_dim", "target_latent_dim", "sem_latent_dim", "MAX_NUM_PARTS", "device",

@@ -399,13 +399,16 @@ def resample_parts(x, labels, k, n=1024, seed=0):
 class PseudoLabelLoader:
     """DataLoader(partnet_dataset) + get_labels (engine/train.py:167-197,
     dataset/dataset_utils.py:1101-1143) on a fixed synthetic target set: cfg["num_targets"]
-    targets (SURVEY §8(d) generator), their part clouds scored against every source by calc_dcd
-    once on the GPU (PairGenerator.cross: the per-part pickle rows of generate_pair.py), and
-    the labels chosen by the reference's rule on the device (PseudoLabelTable: top-10 by cd_m,
-    < filter_threshold, semantic preference, mask_label over dist_src's cd_m with cl_k). The
-    table is deterministic, so the labels of every target are computed once and kept on the
-    host (the unique-source tables of a batch are then built without a device sync). Epochs
-    visit the targets in a seeded shuffle (drop_last, as the reference's DataLoader)."""
+    targets (cfg["synthetic_targets"]: "sources" (default) assembles each from distinct source
+    parts, synthetic.make_targets_from_sources; "ball" uses the SURVEY §8(d) generator), their part
+    clouds scored against every source by calc_dcd once on the GPU (PairGenerator.cross: the
+    per-part pickle rows of generate_pair.py), and each batch's labels chosen by the reference's
+    rule on the device (PseudoLabelTable: top-10 by cd_m, < filter_threshold, semantic preference,
+    mask_label over dist_src's cd_m with cl_k) when the batch is drawn, as get_labels runs per
+    iteration. The labels come back to the host (the reference's get_labels returns host arrays,
+    and the distinct-source tables and the graph key are built from them); the next batch's labels
+    are computed on a side stream while the current step runs. Epochs visit the targets in a
+    seeded shuffle ("train" mode; loader_batching), drop_last as the reference's DataLoader."""
 
     def __init__(self, cfg, db, device, dist_src, seed=0):
         from engine.generate_pair import PairGenerator, normalize_pts
@@ -415,10 +418,18 @@ class PseudoLabelLoader:
         T = int(cfg.get("num_targets", 128))
         self.bs, self.shuffle = loader_batching(cfg)
         if T < self.bs:
-            raise ValueError(f"num_targets ({T}) < batch_size ({self.bs}): every epoch would be empty "
+            raise ValueError(f"num_targets ({T}) < batch size ({self.bs}): every epoch would be empty "
                              "(the reference's DataLoader drops the last partial batch)")
-        t = synthetic.make_batch(T, cfg.get("num_points", 2048), db.num_sources, max_parts=P,
-                                 parts=cfg.get("parts", 4), seed=seed * 7777 + 17)
+        kind = cfg.get("synthetic_targets", "sources")
+        if kind == "sources":
+            t = synthetic.make_targets_from_sources(db.points.cpu().numpy(), db.sem.cpu().numpy(), T,
+                                                    cfg.get("num_points", 2048), parts=cfg.get("parts", 4),
+                                                    seed=seed * 7777 + 17)
+        elif kind == "ball":
+            t = synthetic.make_batch(T, cfg.get("num_points", 2048), db.num_sources, max_parts=P,
+                                     parts=cfg.get("parts", 4), seed=seed * 7777 + 17)
+        else:
+            raise ValueError(f"synthetic_targets: 'sources' or 'ball', got {kind!r}")
         self.targets = t
         rows = np.full((T, P), -1, np.int64)
         clouds, part_sem = [], []
@@ -435,22 +446,41 @@ class PseudoLabelLoader:
                                       alpha=cfg.get("filter_threshold", 2e-2), cl_k=cfg.get("cl_k", 40),
                                       device=device)
         self.part_rows = rows
-        self.labels = self.table.labels(torch.from_numpy(rows).to(device)).cpu().numpy()
+        self._rows_dev = torch.from_numpy(rows).to(device)
+        self._side = torch.cuda.Stream(device=device) if torch.device(device).type == "cuda" else None
         self.n = T // self.bs
         self.epoch = 0
+        self.last_sel = None
 
     def __len__(self):
         return self.n
+
+    def _labels_async(self, sel):
+        """get_labels of the targets `sel` on the side stream -> (pinned host tensor, event)."""
+        with torch.cuda.stream(self._side):
+            idx = upload(np.asarray(sel, np.int64), self.device)
+            lab = self.table.labels(self._rows_dev.index_select(0, idx))
+            host = torch.empty(lab.shape, dtype=lab.dtype, pin_memory=True)
+            host.copy_(lab, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        return host, ev
 
     def __iter__(self):
         rng = np.random.Generator(np.random.PCG64([self.seed, self.epoch]))
         self.epoch += 1
         T = self.targets["x"].shape[0]
         order = rng.permutation(T) if self.shuffle else np.arange(T)
-        for i in range(self.n):
-            sel = order[i * self.bs:(i + 1) * self.bs]
+        sels = [order[i * self.bs:(i + 1) * self.bs] for i in range(self.n)]
+        pending = self._labels_async(sels[0]) if sels else None
+        for i, sel in enumerate(sels):
+            host, ev = pending
+            if i + 1 < len(sels):
+                pending = self._labels_async(sels[i + 1])       # overlaps this batch's step
+            ev.synchronize()
             b = {"x": self.targets["x"][sel], "labels": self.targets["labels"][sel],
-                 "tgt_sem": self.targets["tgt_sem"][sel], "src_labels": self.labels[sel]}
+                 "tgt_sem": self.targets["tgt_sem"][sel], "src_labels": host.numpy().copy()}
+            self.last_sel = sel
             yield batch_to_device(b, self.device, self.db.num_sources,
                                   bucket=8 if self.cfg.get("cuda_graph") else None)
 

@@ -64,8 +64,11 @@ class TargetEncoder(nn.Module):
                                            nn.Conv1d(embedding_size, embedding_size, 1))
         self.fc = nn.Linear(1024, embedding_size)
         # parity diagnostics: when set, forward keeps the max-pool winners (last_pool_idx [G, 1024])
+        # and the values they were chosen from (last_pool_vals: fuse_sem's raw output [G*n, 1024] and
+        # its BatchNorm scale / shift; the pooled activation is relu(y * scale + shift))
         self.record_pool = False
         self.last_pool_idx = None
+        self.last_pool_vals = None
 
     def _layers(self):
         convs = [(self.mlp1[0], self.mlp1[1]), (self.mlp1[3], self.mlp1[4]), (self.mlp2[0], self.mlp2[1]),
@@ -99,6 +102,7 @@ class TargetEncoder(nn.Module):
         if rec is not None:       # the max-pool winner of every (group, channel), within its group
             G = rec["pool_rows"].shape[0]
             self.last_pool_idx = rec["pool_rows"].long() - n * torch.arange(G, device=xf.device).unsqueeze(1)
+            self.last_pool_vals = (rec["pool_y"], rec["pool_scale"], rec["pool_shift"], n)
         return code, pp
 
     def forward(self, x, sem_f):

@@ -123,8 +123,10 @@ class PointEncoderFn(Function):
         K.gemm(G, C, pooled.shape[1], pooled, pooled.shape[1], fcW, fcW.shape[1], code, C, bias=fcb)
         ctx.spec = spec
         ctx.states = states
-        if spec.record is not None:      # diagnostics / parity tests: the max-pool winners
-            spec.record["pool_rows"] = argidx
+        if spec.record is not None:      # diagnostics / parity tests: the max-pool winners and the
+            spec.record["pool_rows"] = argidx        # values they were chosen from (relu(Y*scale+shift))
+            spec.record["pool_y"], spec.record["pool_scale"], spec.record["pool_shift"] = \
+                Ys[5], states[5].scale, states[5].shift
         ctx.save_for_backward(x, sem, pooled, argidx, *Ys, *params)
         return code, pp
 

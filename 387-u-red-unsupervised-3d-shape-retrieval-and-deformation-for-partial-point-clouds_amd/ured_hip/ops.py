@@ -302,6 +302,7 @@ class UniqueRows:
         uniq, inv, cnt = np.unique(idx, return_inverse=True, return_counts=True)
         order = np.argsort(inv, kind="stable")
         off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
+        self.U_distinct = int(uniq.shape[0])
         if bucket:
             pad = min(-(-uniq.shape[0] // bucket) * bucket, s.shape[0]) - uniq.shape[0]
             if pad > 0:
@@ -322,7 +323,7 @@ class UniqueRows:
 
     def clone(self):
         c = UniqueRows.__new__(UniqueRows)
-        c.U = self.U
+        c.U, c.U_distinct = self.U, self.U_distinct
         for f in self.FIELDS:
             setattr(c, f, getattr(self, f).clone())
         return c

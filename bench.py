@@ -412,18 +412,49 @@ def pair_rate(dev, parts=512, pts=1024):
             "pairs_per_s": round(npairs / t, 1), "gpair_dist_s": round(npairs * pts * pts / t / 1e9, 1)}
 
 
-def loader_rate(step, cfg, db, dev, steps, world=1, rank=0, warm_epochs=2):
+class GemmFlops:
+    """Sum of 2MNK over the ured_gemm launches issued inside the context (no timing)."""
+
+    def __enter__(self):
+        from ured_hip import kernels
+        self.k, self.orig, self.flop = kernels, kernels.gemm, 0.0
+
+        def counted(M, N, K, *a, **kw):
+            if variant_key(kw, M, N, K) is not None:     # the split-K store path counts once
+                self.flop += 2.0 * M * N * K
+            return self.orig(M, N, K, *a, **kw)
+        kernels.gemm = counted
+        return self
+
+    def __exit__(self, *exc):
+        self.k.gemm = self.orig
+
+
+def batch_workload(eager, batch, num_sources):
+    """(distinct source parts encoded, padded count, GEMM TFLOP) of one step on `batch` (one eager
+    step outside any timed region)."""
+    s = batch["src_unique"]
+    with GemmFlops() as gf:
+        eager.step(batch)
+    return s.U_distinct, s.U, gf.flop / 1e12
+
+
+def loader_rate(step, eager, cfg, db, dev, steps, world=1, rank=0, warm_epochs=2, head_batches=None):
     """The reference's per-iteration data path inside the timed loop (engine/train.py:190-232):
     every step takes its batch from engine/train.py's PseudoLabelLoader — a seeded shuffle of a
-    fixed synthetic target set whose source labels are the reference's get_labels rule evaluated
-    on the device over a calc_dcd table (PseudoLabelTable) — builds the batch's distinct-source
-    tables on the host and uploads it from pinned host memory (asynchronous copies on the step's
-    stream), then runs the same step as the headline (graph replay at N=1). Warm-up: whole epochs,
-    so the graphs of the batch shapes an epoch produces are captured before timing."""
+    fixed synthetic target set assembled from source parts (4 per target, as the headline), whose
+    source labels the reference's get_labels rule picks on the device over a calc_dcd table
+    (PseudoLabelTable) when the batch is drawn — copies the labels back to the host (as
+    get_labels returns them), builds the batch's distinct-source tables there and uploads it from
+    pinned host memory, then runs the same step as the headline (graph replay at N=1; the loader
+    pads the distinct-source count to a multiple of 8 so that an epoch needs few graphs). Warm-up:
+    whole epochs, so the graphs of the batch shapes an epoch produces are captured before timing.
+    Reported beside the rate: the distinct source parts per step and the GEMM TFLOP per step of the
+    loader's batches and of the headline's."""
     from engine.train import PseudoLabelLoader
     from train_utils.load_sources import source_connectivity
     dist_src = source_connectivity(db)[2]
-    lcfg = dict(cfg, num_targets=max(128, 8 * cfg["batch_size"]))
+    lcfg = dict(cfg, num_targets=max(128, 8 * cfg["batch_size"]), synthetic_targets="sources")
     ld = PseudoLabelLoader(lcfg, db, dev, dist_src, seed=17 + rank)
 
     def batches():
@@ -432,24 +463,38 @@ def loader_rate(step, cfg, db, dev, steps, world=1, rank=0, warm_epochs=2):
     it = batches()
     for _ in range(warm_epochs * len(ld)):
         step.step(next(it))
-    graphs0 = len(getattr(step, "graphs", {}))
+    graphs0 = getattr(step, "captures", 0)
+    us, ups = [], []
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step.step(next(it))
+        bt = next(it)
+        us.append(bt["src_unique"].U_distinct)
+        ups.append(bt["src_unique"].U)
+        step.step(bt)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     tt = torch.tensor([time.perf_counter() - t0], device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    # the workload of both batch streams, outside the timed loop: one eager step per batch
+    lw = [batch_workload(eager, next(it), db.num_sources) for _ in range(4)]
+    hw = [batch_workload(eager, b, db.num_sources) for b in (head_batches or [])]
+    mean = lambda v: round(float(np.mean(v)), 2) if v else None      # noqa: E731
     return {"iters_s": round(steps * world / float(tt.item()), 4), "steps": steps,
-            "graphs_captured_in_timed_steps": len(getattr(step, "graphs", {})) - graphs0,
+            "graphs_captured_in_timed_steps": getattr(step, "captures", 0) - graphs0,
             "num_targets": lcfg["num_targets"],
-            "what": "each step: PseudoLabelLoader batch (get_labels rule on a device calc_dcd table, "
-                    "host distinct-source tables) + pinned-memory upload inside the timed loop"}
+            "distinct_sources_per_step": mean(us), "padded_sources_per_step": mean(ups),
+            "gemm_tflop_per_step": mean([w[2] for w in lw]),
+            "headline_distinct_sources_per_step": mean([w[0] for w in hw]),
+            "headline_padded_sources_per_step": mean([w[1] for w in hw]),
+            "headline_gemm_tflop_per_step": mean([w[2] for w in hw]),
+            "what": "each step: PseudoLabelLoader batch (targets assembled from source parts, 4 per target; the "
+                    "get_labels rule evaluated on the device over a calc_dcd table when the batch is drawn, labels "
+                    "copied to the host, host distinct-source tables) + pinned-memory upload inside the timed loop"}
 
 
 def _free_port():
@@ -657,7 +702,8 @@ def main():
         cfg["unique_sources"] = True
     loader = None
     if not args.no_loader_rate and not args.no_extras:
-        loader = loader_rate(step, dict(cfg, unique_sources=True), db, dev, args.steps, world, rank)
+        loader = loader_rate(step, eager, dict(cfg, unique_sources=True), db, dev, args.steps, world, rank,
+                             head_batches=batches)
     k16_rate = None
     if not args.no_k16_rate and args.parts != 16:
         # SURVEY §8(d)'s stress case: 16 parts per target, no padding slots (~200 distinct sources)

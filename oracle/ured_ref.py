@@ -165,39 +165,55 @@ def bn(x, P, name, training=True):
                         P[name + ".weight"], P[name + ".bias"], training, BN_MOMENTUM, BN_EPS)
 
 
-POOL_TIE_TOL = 1e-4
+U32 = 2.0 ** -24          # fp32 unit roundoff
 
 
-def max_pool(h, pool_idx=None, record=None, tie_tol=POOL_TIE_TOL):
+def max_pool(h, pool_idx=None, record=None, gpu_h=None):
     """max_pool1d over points (simple_encoder.py:105): h [G, C, N] -> [G, C].
 
-    pool_idx (optional, [G, C] point index per channel): the winners another implementation
-    chose; they are taken instead of the argmax, after checking that each is a max up to
-    tie_tol of its channel's scale (an fp32 near-tie resolved the other way, not a wrong
-    point) — parity tests then compare gradients routed to the same points. record: gets
-    "argmax" (this function's own winners) and "overridden" (how many winners were taken)."""
+    pool_idx (optional, [G, C] point index per channel): the winners another implementation (the
+    HIP step) chose; they are taken instead of this function's argmax after a check derived from
+    that implementation's own values, gpu_h(pidx [G, C]) -> its activation at those points: its
+    winner w is a maximum of ITS values (ties to the lowest point), so with m this function's
+    argmax, h[m] - h[w] = (h[m] - h_gpu[m]) + (h_gpu[m] - h_gpu[w]) + (h_gpu[w] - h[w]) <=
+    |h[m] - h_gpu[m]| + |h_gpu[w] - h[w]|: the gap between the two choices may not exceed the two
+    points' fp32 deviations (+ a few ulp of the channel's values). Anything wider is a wrong
+    winner and raises. record gets "argmax" and the tie statistics: "overridden", "exact_ties"
+    (gap exactly 0: e.g. channels whose ReLU output is 0 at both points), "near_ties",
+    "max_gap" (absolute), "max_gap_rel" (over the channel's max |h|), "max_gap_over_bound"."""
     mx, am = h.max(dim=2)
     if record is not None:
         record["argmax"] = am.detach()
     if pool_idx is None:
         return mx
+    if gpu_h is None:
+        raise ValueError("max_pool: pool_idx needs gpu_h (the other implementation's values) for the tie check")
     idx = pool_idx.to(am.device).long()
     chosen = h.gather(2, idx.unsqueeze(-1)).squeeze(-1)
-    scale = h.detach().abs().amax(dim=2) + 1e-12
     gap = (mx - chosen).detach()
-    bad = gap > tie_tol * scale
+    hd = h.detach()
+    bound = ((gpu_h(idx).to(hd.dtype) - chosen.detach()).abs() + (gpu_h(am).to(hd.dtype) - mx.detach()).abs()
+             + 4 * U32 * (mx.detach().abs() + chosen.detach().abs()))
+    over = idx != am
+    bad = gap > bound
     if bool(bad.any()):
         g, c = [int(v) for v in bad.nonzero()[0]]
-        raise AssertionError(f"max-pool winner {int(idx[g, c])} of group {g} channel {c} is "
-                             f"{float(gap[g, c]):.3e} below the max ({float(mx[g, c]):.6e}): not a near-tie")
+        raise AssertionError(f"max-pool winner {int(idx[g, c])} of group {g} channel {c} is {float(gap[g, c]):.3e} "
+                             f"below the max ({float(mx[g, c]):.6e}), beyond the fp32 deviation bound "
+                             f"{float(bound[g, c]):.3e}: not a near-tie")
     if record is not None:
-        record["overridden"] = int((idx != am).sum())
+        scale = hd.abs().amax(dim=2) + 1e-30
+        g_o = gap[over]
+        record.update(overridden=int(over.sum()), exact_ties=int((g_o == 0).sum()), near_ties=int((g_o > 0).sum()),
+                      max_gap=float(g_o.max()) if g_o.numel() else 0.0,
+                      max_gap_rel=float((gap / scale)[over].max()) if g_o.numel() else 0.0,
+                      max_gap_over_bound=float((gap / (bound + 1e-300))[over].max()) if g_o.numel() else 0.0)
     return chosen
 
 
-def target_encoder(P, x, sem_f, is_src, training=True, pool_idx=None, record=None):
+def target_encoder(P, x, sem_f, is_src, training=True, pool_idx=None, record=None, gpu_h=None):
     """network/simple_encoder.py:88-107. x: [B,N,3] (tgt) or [B,P,N,3] (src). pool_idx /
-    record: see max_pool."""
+    record / gpu_h: see max_pool."""
     if is_src:
         B, Pn, N, _ = x.shape
         x = x.reshape(B * Pn, N, 3)
@@ -216,7 +232,7 @@ def target_encoder(P, x, sem_f, is_src, training=True, pool_idx=None, record=Non
     h = F.relu(bn(conv(h, P, "fuse_sem.0"), P, "fuse_sem.1", training))
     pp = F.relu(bn(conv(h, P, "per_point_out.0"), P, "per_point_out.1", training))
     pp = conv(pp, P, "per_point_out.3")
-    g = max_pool(h, pool_idx, record)
+    g = max_pool(h, pool_idx, record, gpu_h)
     g = F.linear(g, P["fc.weight"], P["fc.bias"])
     return g, pp
 
@@ -320,7 +336,37 @@ def get_symmetric(pc):
     return torch.cat([-pc[:, :, :1], pc[:, :, 1:2], pc[:, :, 2:3]], dim=2)
 
 
-NN_TIE_TOL = 1e-4
+NN_TIE_STATS = {}          # filled by the index checks below; reset / read by the parity tests
+
+
+def _nn_stat(name, over, exact, ratio):
+    st = NN_TIE_STATS.setdefault(name, {"overridden": 0, "exact_ties": 0, "near_ties": 0, "max_over_bound": 0.0})
+    st["overridden"] += int(over.sum())
+    st["exact_ties"] += int((over & exact).sum())
+    st["near_ties"] += int((over & ~exact).sum())
+    if bool(over.any()):
+        st["max_over_bound"] = max(st["max_over_bound"], float(ratio[over].max()))
+
+
+def check_nn_choice(P_q, P_c, j_given, j_own, delta_q, delta_c, name):
+    """NN indices chosen by another implementation from its own copy q of one point set (the HIP
+    step's fp32 deformed shape), checked against the nearest neighbours here: for query i the
+    given candidate j must satisfy |P_q[i] - P_c[j]| <= (d_i + dq_i + dc)(1 + 4u) + dq_i + dc,
+    with d_i = |P_q[i] - P_c[own]|, dq_i = |q_i - P_q[i]| when the queries are the copied set,
+    dc = max_k |q_k - P_c[k]| when the candidates are (the triangle inequality around the other
+    implementation's own argmin, plus its fp32 distance rounding). P_q [B, n, 3], P_c [B, m, 3]
+    float64; j_given / j_own [B, n] int; delta_q [B, n] or 0; delta_c [B] or 0."""
+    bi = torch.arange(P_q.shape[0]).unsqueeze(1)
+    e = (P_q - P_c[bi, j_given]).norm(dim=-1)
+    d = (P_q - P_c[bi, j_own]).norm(dim=-1)
+    dq = delta_q if torch.is_tensor(delta_q) else torch.zeros_like(d)
+    dc = delta_c.unsqueeze(1) if torch.is_tensor(delta_c) else torch.zeros_like(d)
+    bound = (d + dq + dc) * (1 + 4 * U32) + dq + dc
+    over = j_given != j_own
+    if bool((e > bound).any()):
+        raise AssertionError(f"given NN index ({name}) is {float((e - bound).max()):.3e} farther than the "
+                             "fp32 deviation bound around the nearest point: not a near-tie")
+    _nn_stat(name, over, e == d, (e - d) / (bound - d + 1e-300))
 
 
 class _OracleNN(torch.autograd.Function):
@@ -328,27 +374,24 @@ class _OracleNN(torch.autograd.Function):
 
     q1 (optional): another copy of p1 (e.g. the HIP step's fp32 deformed shape) from which the
     NN indices of both directions are taken instead of p1's own. The distances are then those
-    of p1 / p2 at these indices, each checked to be the minimum up to NN_TIE_TOL (a near-tie
-    resolved the other way by the inputs' fp32-level differences, not a wrong neighbour), so a
-    parity test compares gradients routed to the same points."""
+    of p1 / p2 at these indices, each checked (check_nn_choice) to be the minimum up to the two
+    copies' deviation, so a parity test compares gradients routed to the same points."""
 
     @staticmethod
     def forward(ctx, p1, p2, q1=None):
         a, b = p1.detach().float().numpy(), p2.detach().float().numpy()
         d1, d2, i1, i2 = nn_ref.nn_fwd(a, b)
         if q1 is not None:
-            _, _, i1, i2 = nn_ref.nn_fwd(np.ascontiguousarray(q1.detach().float().numpy()), b)
-            P1, P2 = p1.detach(), p2.detach()
+            _, _, g1, g2 = nn_ref.nn_fwd(np.ascontiguousarray(q1.detach().float().numpy()), b)
+            P1, P2 = p1.detach().double(), p2.detach().double()
+            dev = (q1.detach().double() - P1).norm(dim=-1)                  # [B, n]
+            t = lambda v: torch.from_numpy(np.asarray(v)).long()           # noqa: E731
+            check_nn_choice(P1, P2, t(g1), t(i1), dev, 0, "p1 -> p2")
+            check_nn_choice(P2, P1, t(g2), t(i2), 0, dev.amax(dim=1), "p2 -> p1")
+            i1, i2 = g1, g2
             bi = torch.arange(P1.shape[0]).unsqueeze(1)
-            e1 = ((P1 - P2[bi, torch.from_numpy(i1).long()]) ** 2).sum(-1)
-            e2 = ((P2 - P1[bi, torch.from_numpy(i2).long()]) ** 2).sum(-1)
-            for e, d, name in ((e1, d1, "p1 -> p2"), (e2, d2, "p2 -> p1")):
-                dd = torch.from_numpy(d).to(e.dtype)
-                bad = e > dd * (1 + NN_TIE_TOL) + 1e-10
-                if bool(bad.any()):
-                    raise AssertionError(f"given NN index ({name}) is {float((e - dd)[bad].max()):.3e} farther than "
-                                         "the nearest point: not a near-tie")
-            d1, d2 = e1.numpy(), e2.numpy()
+            d1 = ((p1.detach() - p2.detach()[bi, t(i1)]) ** 2).sum(-1).numpy()
+            d2 = ((p2.detach() - p1.detach()[bi, t(i2)]) ** 2).sum(-1).numpy()
         ctx.save_for_backward(p1, p2)
         ctx.idx = (i1, i2)
         return torch.from_numpy(np.asarray(d1)).to(p1.dtype), torch.from_numpy(np.asarray(d2)).to(p1.dtype)
@@ -400,13 +443,13 @@ def residual_retrieval_loss(x, x_source, residuals, mask, np_per_part=1024, sour
         xs = x[b].detach().float().numpy()
         _, idx = nn_ref.nn_dir(xs, src.float().numpy())
         if source_q is not None:
-            qs = np.ascontiguousarray(source_q[b, :int(n_valid[b].item())].detach().float().numpy())
-            d_own, _ = nn_ref.nn_dir(xs, src.float().numpy())
-            _, idx = nn_ref.nn_dir(xs, qs)
-            e = ((x[b].detach() - src[torch.from_numpy(idx).long()]) ** 2).sum(-1)
-            dd = torch.from_numpy(d_own).to(e.dtype)
-            if bool((e > dd * (1 + NN_TIE_TOL) + 1e-10).any()):
-                raise AssertionError("given kNN index is not a near-tie of the nearest point")
+            qb = source_q[b, :int(n_valid[b].item())].detach()
+            own = idx
+            _, idx = nn_ref.nn_dir(xs, np.ascontiguousarray(qb.float().numpy()))
+            dc = (qb.double() - src.double()).norm(dim=-1).amax().reshape(1)
+            check_nn_choice(x[b:b + 1].detach().double(), src.double().unsqueeze(0),
+                            torch.from_numpy(idx).long().unsqueeze(0), torch.from_numpy(own).long().unsqueeze(0),
+                            0, dc, "kNN x -> out")
         nns.append(src[torch.from_numpy(idx).long()])
     nn = torch.stack(nns)
     res = x + residuals - nn
@@ -469,15 +512,17 @@ def train_forward(params, batch, cfg, training=True, epoch=0):
     B = x.shape[0]
 
     pool = batch.get("_pool_idx", {})      # optional max-pool winners to follow (see max_pool)
+    pvals = batch.get("_pool_gpu", {})     # ... and the values they were chosen from
     prec = {"src_encoder_all": {}, "target_encoder_full": {}}
     codes, src_pp = target_encoder(params["src_encoder_all"], src_pts, src_sem_f, True, training,
-                                   pool.get("src_encoder_all"), prec["src_encoder_all"])
+                                   pool.get("src_encoder_all"), prec["src_encoder_all"], pvals.get("src_encoder_all"))
     rin = torch.cat([codes.unsqueeze(2).expand(-1, -1, src_pp.shape[-1]), src_pp], dim=1)
     recon_src = residual_net(params["recon_decoder_src"], rin.permute(0, 2, 1), training)
     recon_src = recon_src.reshape(B, P_max, -1, 3)
 
     tcode, pp = target_encoder(params["target_encoder_full"], x, tgt_sem_f, False, training,
-                               pool.get("target_encoder_full"), prec["target_encoder_full"])
+                               pool.get("target_encoder_full"), prec["target_encoder_full"],
+                               pvals.get("target_encoder_full"))
     pp = pp.permute(0, 2, 1)
     part_f, re_in, mask, part_x, param_def = get_part(pp, batch["labels"], x, P_max)
     N = pp.shape[1]

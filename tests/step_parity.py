@@ -51,6 +51,47 @@ def gpu_pool_choices(models, batch, unique):
     return out
 
 
+def gpu_pool_values(models, batch, unique):
+    """{encoder: gpu_h} for ured_ref.max_pool: gpu_h(pidx [groups, 1024]) -> the HIP step's pooled
+    activation relu(y * scale + shift) (fp32, as its kernels compute it) at point pidx[g, c] of
+    group g, channel c, in the oracle's grouping (unique-source encoding: slot s reads the
+    distinct part inverse[s])."""
+    out = {}
+    for name in ENCODERS:
+        y, sc, sh, n = models[name].last_pool_vals
+        y, sc, sh = y.detach().cpu(), sc.detach().cpu(), sh.detach().cpu()
+        grp = None
+        if name == "src_encoder_all" and unique:
+            grp = batch["src_unique"].inverse.cpu()
+
+        def gpu_h(pidx, y=y, sc=sc, sh=sh, n=n, grp=grp):
+            G, C = pidx.shape
+            g = torch.arange(G).unsqueeze(1) if grp is None else grp.unsqueeze(1)
+            rows = g * n + pidx.long()
+            v = y[rows, torch.arange(C).unsqueeze(0)]
+            return torch.relu(torch.addcmul(sh.unsqueeze(0), v, sc.unsqueeze(0))).double()
+        out[name] = gpu_h
+    return out
+
+
+def tie_report(pool_rec, label=""):
+    """Prints the max-pool and NN tie statistics of one oracle run (ured_ref.max_pool records,
+    ured_ref.NN_TIE_STATS): winners taken from the HIP step, exact ties (equal values) vs near-ties,
+    and the largest gap, absolute / relative to the channel / relative to its fp32 bound."""
+    from oracle import ured_ref
+    parts = []
+    for n in ENCODERS:
+        r = pool_rec[n]
+        if "overridden" in r:
+            parts.append(f"{n}: {r['overridden']} overridden ({r['exact_ties']} exact ties, {r['near_ties']} near-ties), "
+                         f"max gap {r['max_gap']:.2e} ({r['max_gap_rel']:.2e} of the channel max, "
+                         f"{r['max_gap_over_bound']:.2f} of the fp32 bound)")
+    for k, st in sorted(ured_ref.NN_TIE_STATS.items()):
+        parts.append(f"NN {k}: {st['overridden']} overridden ({st['exact_ties']} exact, {st['near_ties']} near), "
+                     f"max {st['max_over_bound']:.2f} of the bound")
+    print(f"\n{label} ties: " + "; ".join(parts))
+
+
 def same_pools(choices, oracle_pool):
     """True when the GPU's winners are the oracle's own argmax everywhere."""
     return all(torch.equal(choices[n].long(), oracle_pool[n]["argmax"].long().cpu()) for n in ENCODERS)

@@ -39,10 +39,18 @@ def test_pseudo_label_loader_matches_get_labels(dev, tmp_path):
     lists = [[int(r) for r in row if r >= 0] for row in rows]
     exp = ref.get_labels(lists, ld.table.cd_m.cpu().numpy(), ld.table.part_sem.cpu().numpy(), db.sem.cpu().numpy(),
                          dist_src, cfg["filter_threshold"], cfg["cl_k"], cfg["MAX_NUM_PARTS"])
-    np.testing.assert_array_equal(ld.labels, exp)
+    got = ld.table.labels(torch.from_numpy(rows).to(dev)).cpu().numpy()
+    np.testing.assert_array_equal(got, exp)
     assert (exp[:, :3] >= 0).any()
-    batches = list(ld)
-    assert len(batches) == 3 and all(b["x"].shape == (2, 256, 3) for b in batches)
+    n = 0
+    for b in ld:                        # each batch's labels drawn on the device when it is drawn
+        assert b["x"].shape == (2, 256, 3)
+        np.testing.assert_array_equal(b["src_labels"].cpu().numpy(), exp[ld.last_sel])
+        n += 1
+    assert n == 3
+    # targets assembled from source parts: most parts are labelled with their own source
+    own = ld.targets["src_true"]
+    assert (exp[own >= 0] == own[own >= 0]).mean() > 0.5
 
 
 def test_train_then_test_main(dev, tmp_path):

@@ -103,7 +103,7 @@ def _oracle_floor(key, cfg, db_np, bt):
     return _ORACLE[key]
 
 
-def _oracle64(cfg, db_np, bt, pool_idx=None, nn_out=None):
+def _oracle64(cfg, db_np, bt, pool_idx=None, nn_out=None, pool_vals=None):
     """float64 oracle forward + backward -> (terms, out, gradients, its max-pool record).
     pool_idx / nn_out: the HIP step's max-pool winners and deformed shape, whose discrete choices
     (max-pool winners, NN indices) the oracle follows where they are near-ties of its own
@@ -113,8 +113,10 @@ def _oracle64(cfg, db_np, bt, pool_idx=None, nn_out=None):
     ob = _oracle_batch(db_np, bt)
     if pool_idx is not None:
         ob["_pool_idx"] = pool_idx
+        ob["_pool_gpu"] = pool_vals
     if nn_out is not None:
         ob["_nn_out"] = nn_out
+    ured_ref.NN_TIE_STATS.clear()
     loss, R = ured_ref.train_forward(P64, ob, cfg)
     loss.backward()
     res = ({k: float(R[k]) for k in TERMS}, R["_out"].detach().float(), _grads_of(P64), R["_pool"])
@@ -152,9 +154,9 @@ def _check_step(dev, B, N, parts, unique):
     label = f"B={B} N={N} k={parts} unique={unique}"
     rgrads32 = _oracle_floor((B, N, parts), cfg, db_np, bt)
     choices = step_parity.gpu_pool_choices(ts.models, batch, unique)
-    rterms, rout, rgrads, rpool = _oracle64(cfg, db_np, bt, choices, out.cpu())
-    print(f"\n{label}: max-pool winners taken from the HIP step where they differ (ties): " +
-          ", ".join(f"{n} {rpool[n]['overridden']}" for n in step_parity.ENCODERS))
+    vals = step_parity.gpu_pool_values(ts.models, batch, unique)
+    rterms, rout, rgrads, rpool = _oracle64(cfg, db_np, bt, choices, out.cpu(), vals)
+    step_parity.tie_report(rpool, label)
     step_parity.check_loss_terms(got_terms, rterms, label)
     o = out.cpu()
     assert (o - rout).abs().max().item() <= 1e-4 * rout.abs().max().item()

@@ -92,9 +92,12 @@ def test_train_step_matches_oracle(dev, N, parts, unique):
     # the oracle routes each pooled gradient to the point the HIP step chose (checked to be a
     # max up to fp32 noise: near-ties may resolve either way under a different summation order)
     ob["_pool_idx"] = step_parity.gpu_pool_choices(ts.models, batch, unique)
+    ob["_pool_gpu"] = step_parity.gpu_pool_values(ts.models, batch, unique)
     ob["_nn_out"] = T["_out"].detach().cpu()      # NN indices: the HIP step's near-tie choices too
+    ured_ref.NN_TIE_STATS.clear()
     rloss, R = ured_ref.train_forward(P, ob, cfg)
     label = f"N={N} parts={parts} unique={unique}"
+    step_parity.tie_report(R["_pool"], label)
     step_parity.check_loss_terms({k: T[k].item() for k in TERMS}, {k: R[k].item() for k in TERMS}, label)
     o, ro = T["_out"].detach().cpu(), R["_out"].detach()
     assert (o - ro).abs().max().item() <= 1e-4 * ro.abs().max().item()
@@ -116,8 +119,11 @@ def test_train_step_param_loss_complementme(dev, case):
     step_parity.record_pools(ts.models)
     loss, T = ts.forward(batch)
     ob["_pool_idx"] = step_parity.gpu_pool_choices(ts.models, batch, True)
+    ob["_pool_gpu"] = step_parity.gpu_pool_values(ts.models, batch, True)
     ob["_nn_out"] = T["_out"].detach().cpu()
+    ured_ref.NN_TIE_STATS.clear()
     rloss, R = ured_ref.train_forward(P, ob, cfg)
+    step_parity.tie_report(R["_pool"], case)
     terms = TERMS + (("param_loss",) if "use_param_loss" in over else ())
     assert ("param_loss" in T) == ("use_param_loss" in over)
     step_parity.check_loss_terms({k: T[k].item() for k in terms}, {k: R[k].item() for k in terms}, case)
