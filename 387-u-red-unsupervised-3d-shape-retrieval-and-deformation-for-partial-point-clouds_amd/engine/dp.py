@@ -227,9 +227,17 @@ class FlatGradReducer:
 
 
 class DataParallelStep(TrainStep):
+    """cfg["dp_force_collectives"]: run every collective (bucketed gradient all-reduce, the
+    contrastive all_gather) through the process group even at world size 1 — the test hook that
+    exercises the RCCL code paths, eager and captured, on a one-GPU box."""
+
     def __init__(self, cfg, db, device, bucket_mb=25.0, overlap=None):
         super().__init__(cfg, db, device)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.collect = self.world > 1 or (bool(cfg.get("dp_force_collectives", False)) and dist.is_initialized())
+        if self.collect:
+            import loss.contrast_loss as cl
+            cl.FORCE_GATHER = True
         if self.world > 1:
             self.broadcast_state()
         params = []
@@ -238,9 +246,9 @@ class DataParallelStep(TrainStep):
         self.params = params[::-1]          # ~ the order backward produces gradients
         self.bucket_elems = int(bucket_mb * 1e6 / 4)
         self._buckets = None                # torch-Adam path: (active key, buckets)
-        overlap = (self.world > 1) if overlap is None else bool(overlap)
+        overlap = self.collect if overlap is None else bool(overlap)
         self.reducer = (FlatGradReducer(self.optimizer, params, self.world, self.bucket_elems, overlap)
-                        if self.world > 1 and hasattr(self.optimizer, "prepare") else None)
+                        if self.collect and hasattr(self.optimizer, "prepare") else None)
 
     def broadcast_state(self, src=0):
         """Every rank starts from rank src's parameters and buffers (as DDP's constructor does:
@@ -250,18 +258,12 @@ class DataParallelStep(TrainStep):
                 for t in list(self.models[name].parameters()) + list(self.models[name].buffers()):
                     dist.broadcast(t.data, src)
 
-    def step(self, batch, epoch=0):
-        self.optimizer.zero_grad(set_to_none=True)
-        loss, T = self.forward(batch, epoch)
+    def begin_backward(self):
         if self.reducer is not None:
             self.reducer.begin()
-        loss.backward()
-        self.reduce_gradients()
-        self.clip_and_step()
-        return T
 
     def reduce_gradients(self):
-        if self.world == 1:
+        if not self.collect:
             return
         if self.reducer is not None:
             self.reducer.finish()

@@ -29,14 +29,19 @@ Same kernels, same arithmetic as the eager step: a replay is bit-identical to an
 the same state and batch.
 
 Data parallel (world > 1): the forward contains collectives — the contrastive loss's all_gather
-of the source codes and, with SyncBN, every BN layer's statistics exchange. No collective is
-captured: the fwd_bwd region is captured as a chain of graphs split at each collective
-(ured_hip/collective.py SegmentedCapture), and a replay runs segment, collective, segment, ...
-with the collectives issued eagerly on the segments' static buffers (any backend, gloo
-included). The gradients of the parameters that torch (not a HIP layer) produces are copied
-into their flat-gradient views INSIDE the last segment, so the gradient all-reduce that follows
-the replay (reduce_gradients, eager) reads every gradient of this step and the update graph
-contains no copy that could overwrite the averaged values.
+of the source codes and, with SyncBN, every BN layer's statistics exchange — and the backward
+the bucketed gradient all-reduce.
+  * RCCL ("nccl"): the collectives are captured in the graph (SegmentedCapture(inline=True)): the
+    hooks of engine/dp.py issue each gradient bucket's all-reduce on RCCL's stream as soon as
+    the bucket's last gradient is written, so in the replayed graph the reduction overlaps the
+    rest of the backward, and reduce_gradients() (waits, scaling) is captured after it.
+  * gloo (the CPU / one-GPU rehearsal backend; its collectives cannot be captured): the fwd_bwd
+    region is captured as a chain of graphs split at each collective (ured_hip/collective.py),
+    a replay runs segment, collective, segment, ... with the collectives issued eagerly on the
+    segments' static buffers, and the gradient all-reduce follows the replay. The gradients of
+    the parameters that torch (not a HIP layer) produces are copied into their flat-gradient
+    views INSIDE the last segment, so that all-reduce reads every gradient of this step and the
+    update graph contains no copy that could overwrite the averaged values.
 """
 from collections import OrderedDict
 
@@ -102,6 +107,14 @@ class GraphedStep:
         pb = batch.get("part_bounds")          # sizes the loss head's NN launches (ured_hip/ops.py)
         return (None if uq is None else uq.U, self.gate(epoch), None if pb is None else pb.key())
 
+    def _inline(self):
+        """Capture the collectives inside the graph (RCCL) instead of splitting at them: the
+        contrastive all_gather and the bucketed gradient all-reduce issued from backward's hooks,
+        which then overlaps the rest of the backward on RCCL's stream within one graph."""
+        import torch.distributed as dist
+        return (getattr(self.inner, "collect", False) and dist.is_initialized()
+                and dist.get_backend() == "nccl")
+
     def _flat(self):
         """FlatAdam: the HIP layers write the gradients into its persistent flat buffer."""
         return hasattr(self.inner.optimizer, "flat_grad")
@@ -120,6 +133,7 @@ class GraphedStep:
             return _detached(T)
         self._fresh_grads()
         loss, T = self.inner.forward(batch, epoch)
+        self.inner.begin_backward()
         loss.backward()
         del loss
         self.inner.reduce_gradients()
@@ -134,7 +148,8 @@ class GraphedStep:
         flat = self._flat()
         if flat:
             self.inner.optimizer.zero_grad(set_to_none=True)
-        cap = SegmentedCapture()
+        inline = self._inline()
+        cap = SegmentedCapture(inline=inline)
         stream = torch.cuda.Stream()
         stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(stream):
@@ -143,8 +158,12 @@ class GraphedStep:
                 if not flat:
                     torch._foreach_zero_(self.grads)
                 loss, T = self.inner.forward(static, epoch)
+                if inline:
+                    self.inner.begin_backward()      # bucket all-reduces from the hooks, captured
                 loss.backward()
-                if flat:
+                if inline:
+                    self.inner.reduce_gradients()    # completes the captured reduction (flat views)
+                elif flat:
                     # torch-produced gradients into their flat views, inside the captured region
                     self.inner.optimizer.gather_grads()
             except BaseException:
@@ -161,7 +180,7 @@ class GraphedStep:
         del loss
         if self.g_update is None:
             self._capture_update()
-        self.graphs[key] = (static, cap, T)
+        self.graphs[key] = (static, cap, T, inline)
         while len(self.graphs) > self.max_graphs:
             self.graphs.popitem(last=False)
 
@@ -199,11 +218,12 @@ class GraphedStep:
             self._capture(k, batch, epoch)
             return T
         self.graphs.move_to_end(k)
-        static, cap, T = ent
+        static, cap, T, inline = ent
         for name, v in static.items():
             v.copy_(batch[name], non_blocking=True)
         cap.replay()                         # segments, and the collectives between them
-        self.inner.reduce_gradients()
+        if not inline:
+            self.inner.reduce_gradients()
         sync = getattr(self.inner.optimizer, "sync_lr", None)
         if sync is not None:                 # FlatAdam reads lr from a device scalar
             sync()

@@ -219,7 +219,7 @@ class TrainStep:
         chamfer, contrastive, residual and reconstruction losses and their weighted sum in ~10
         launches forward and ~7 backward (the composed form, _forward_composed, is the same
         arithmetic as ~150 small torch kernels)."""
-        from loss.contrast_loss import get_world_size
+        from loss.contrast_loss import gathers
         from ured_hip.losshead import HeadInputs, loss_head
         cfg, M = self.cfg, self.models
         P = cfg["MAX_NUM_PARTS"]
@@ -248,7 +248,7 @@ class TrainStep:
                                                          off=re_in.off).view(B, N, 3)
         param = regularization_param(params_full, mask_part) if cfg.get("use_param_loss", 0.0) > 0.0 else None
         contrast_ext = None
-        if get_world_size() > 1 and cfg.get("use_contrast_loss", 0.0) > 0.0:
+        if gathers() and cfg.get("use_contrast_loss", 0.0) > 0.0:
             # the reference gathers the source codes of every rank (contrast_loss.py:35-58)
             contrast_labels = torch.where(src_labels >= 0, torch.ones_like(src_labels), src_labels)
             contrast_ext = compute_contrast_loss_loss(target_part_f, codes, contrast_labels,
@@ -338,10 +338,14 @@ class TrainStep:
     def step(self, batch, epoch=0):
         self.optimizer.zero_grad(set_to_none=True)
         loss, T = self.forward(batch, epoch)
+        self.begin_backward()
         loss.backward()
         self.reduce_gradients()
         self.clip_and_step()
         return T
+
+    def begin_backward(self):
+        """Data-parallel hook before loss.backward() (engine/dp.py: arms the bucket all-reduce)."""
 
     def reduce_gradients(self):
         """Data-parallel hook (engine/dp.py overrides); single process: nothing to do."""

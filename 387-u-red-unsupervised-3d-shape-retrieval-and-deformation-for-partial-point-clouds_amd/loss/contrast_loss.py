@@ -25,9 +25,19 @@ def get_rank():
     return dist.get_rank() if is_dist_avail_and_initialized() else 0
 
 
+# engine/dp.py DataParallelStep(cfg["dp_force_collectives"]): gather through the process group even
+# at world size 1 (so a one-GPU box exercises the collective path)
+FORCE_GATHER = False
+
+
+def gathers():
+    """Whether the source codes go through a collective (world > 1, or forced)."""
+    return get_world_size() > 1 or (FORCE_GATHER and is_dist_avail_and_initialized())
+
+
 def all_gather_batch(tensors, differentiable=False):
     world = get_world_size()
-    if world == 1:
+    if not gathers():
         return tensors
     from ured_hip import collective
     out = []

@@ -6,8 +6,11 @@ per-layer statistics exchanges (ured_hip/syncbn.py). Every such call goes throug
 it just issues the collective. While engine/graph.py captures the step, run() instead closes
 the captured segment, records the collective and opens the next segment: a replay is then
 segment 0, collective 0, segment 1, ... — the collectives run eagerly between replays on
-static buffers (no collective is ever captured into a graph, so the capture works with any
-process-group backend, gloo included).
+static buffers (no collective is captured into a graph, so the capture works with any
+process-group backend, gloo included). With RCCL ("nccl"), whose collectives can be captured,
+SegmentedCapture(inline=True) records them in the graph itself: one graph, no split, and the
+bucketed gradient all-reduce issued from backward's hooks is captured with it (overlapping the
+rest of the backward on RCCL's stream, engine/graph.py).
 """
 
 _split = None
@@ -31,9 +34,10 @@ class SegmentedCapture:
         cap.replay()
     """
 
-    def __init__(self, pool=None):
+    def __init__(self, pool=None, inline=False):
         import torch
         self._torch = torch
+        self.inline = inline
         self.pool = pool if pool is not None else torch.cuda.graph_pool_handle()
         self.graphs, self.collectives = [], []
         self._g = None
@@ -59,7 +63,8 @@ class SegmentedCapture:
         if _split is not None:
             raise RuntimeError("nested segmented capture")
         self._open()
-        _split = self._split_at
+        if not self.inline:
+            _split = self._split_at
 
     def end(self):
         global _split
