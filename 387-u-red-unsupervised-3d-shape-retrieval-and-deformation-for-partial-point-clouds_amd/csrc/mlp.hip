@@ -211,15 +211,6 @@ template <bool KM> struct Pad { static constexpr int v = KM ? BM + 4 : BM + 1; }
 #ifndef URED_BNBWD_YALL
 #define URED_BNBWD_YALL 1
 #endif
-// gemm2 BN-backward epilogue: the previous layer's output tile Yp reaches LDS by DMA during the
-// last K-step (rows 0-63 into the free stage buffer, rows 64-127 into the consumed one once every
-// wave has read its fragments), so its HBM latency hides under that step's MFMAs. Measured
-// neutral on the config-2 step (dgrad 3.63 vs 3.56 ms/step, 62.0 vs 62.1 it/s, same-box A/B,
-// tools/gpu_lib_ab.sh): the co-resident block already covers the epilogue's latency. Off; kept
-// for experiments (it lowers the kernel's VGPR count 193 -> 175).
-#ifndef URED_YP_LDS
-#define URED_YP_LDS 0
-#endif
 
 // BN partials (EPI_FWD stat_ws {mean, M2}, EPI_BNBWD bwd_ws {sum g, sum g*xhat}): layout
 // [2][N][nblk], nblk = ceil(M/128) — one column's block partials are contiguous, so the
@@ -379,10 +370,9 @@ __device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2]
     }
 }
 
-template <int EPI, bool BUFST = false, bool YL = false, class Pre = NoPre>
+template <int EPI, bool BUFST = false, class Pre = NoPre>
 __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2], int m0, int n0,
-                                         float* red_f, int* red_i, Pre pre = Pre(),
-                                         const float* yl0 = nullptr, const float* yl1 = nullptr) {
+                                         float* red_f, int* red_i, Pre pre = Pre()) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
     // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
     const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
@@ -574,7 +564,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
     if (EPI == URED_EPI_BNBWD) {
         float s1[2], s2[2];
         const bool pool_al = d.pool_idx && (d.pool_group_rows % BM == 0);
-        const bool full = BUFST && !YL && m0 + BM <= d.M && n0 + BN <= d.N && !d.gadd && (!d.pool_idx || pool_al);
+        const bool full = BUFST && m0 + BM <= d.M && n0 + BN <= d.N && !d.gadd && (!d.pool_idx || pool_al);
         if (full) {
             if (pool_al) {
                 if (d.bwd_res == URED_ACT_RES) bnbwd_full<URED_ACT_RES, true>(d, acc, m0, n0, s1, s2, pre);
@@ -593,9 +583,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         // the fragment registers are dead, so the whole tile fits without raising the kernel's
         // VGPR peak, and the epilogue then waits for one HBM round trip instead of two (gfx9
         // vmcnt is in order: the second half's loads otherwise queue behind the first half's stores)
-        // YL: the tile's Yp rows are in LDS (yl0: rows 0-63, yl1: rows 64-127; 128 floats per row)
-        constexpr bool YG = !YL;               // Yp read from global into registers
-        f16v yh[(URED_BNBWD_YALL || !YG) ? 2 : 1][2];
+        f16v yh[URED_BNBWD_YALL ? 2 : 1][2];
         InTile<BUFST> Yr(d.Yp, d.ldy, d.M, d.N);
         auto load_y = [&](int j) {
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
@@ -604,7 +592,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
 #pragma unroll
                 for (int r = 0; r < 16; ++r) yh[URED_BNBWD_YALL ? j : 0][i][r] = Yr.get(row_of(i, r), col);
         };
-        if (YG && !URED_BNBWD_YALL) load_y(0);
+        if (!URED_BNBWD_YALL) load_y(0);
         // max-pool backward: the pooled gradient lands on the winning row of each (group, column)
         const bool pool_blk = d.pool_idx && (d.pool_group_rows % BM == 0);
         const int pg = pool_blk ? m0 / d.pool_group_rows : 0;
@@ -619,21 +607,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             pidx_[j] = -1; pgr_[j] = 0.f;
             if (pool_blk && cv) { pidx_[j] = d.pool_idx[(size_t)pg * d.N + col]; pgr_[j] = d.pool_grad[(size_t)pg * d.N + col]; }
         }
-        if (YG && URED_BNBWD_YALL) { load_y(0); load_y(1); }   // behind the (L2-resident) per-column parameters
-        if constexpr (YL) {
-            // this wave's Yp DMA (and the parameters) landed, then every wave's
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_barrier();
-            const float* yb = wm ? yl1 : yl0;
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        yh[j][i][r] = yb[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * BN + wn * 64 + j * 32 +
-                                         (lane & 31)];
-        }
+        if (URED_BNBWD_YALL) { load_y(0); load_y(1); }   // behind the (L2-resident) per-column parameters
         pre();
         OutTile<BUFST> Gw(d.C, d.ldc, d.M, d.N);
         // per-element global reads (a residual gradient, or pooled gradients of groups that do
@@ -643,7 +617,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         const float ylo = d.bwd_res == URED_ACT_RES ? 0.f : -__builtin_inff();
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            if (YG && !URED_BNBWD_YALL && j == 1) load_y(1);
+            if (!URED_BNBWD_YALL && j == 1) load_y(1);
             const int col = n0 + wn * 64 + j * 32 + (lane & 31);
             const bool cv = col < d.N;
             const float sc = sc_[j], sh = sh_[j], mu = mu_[j], is = is_[j];
@@ -663,7 +637,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                         const bool ok = cv && row < d.M;
                         const float a = acc[i][j][r];
                         const float dh = (row == pidx) ? a + pgr : a;
-                        const float y = yh[(URED_BNBWD_YALL || YL) ? j : 0][i][r];
+                        const float y = yh[URED_BNBWD_YALL ? j : 0][i][r];
                         const float xh = (fmaxf(y, ylo) - mu) * is;
                         const float g = (__builtin_fmaf(y, sck, shk) > 0.f) ? dh : 0.f;
                         Gw.put(ok, row, col, g);
@@ -685,7 +659,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                         if (d.pool_idx[ge] == row) dh += d.pool_grad[ge];
                     }
                     if (d.gadd && ok) dh += d.gadd[(size_t)row * d.ldg + col];
-                    const float y = yh[(URED_BNBWD_YALL || YL) ? j : 0][i][r];
+                    const float y = yh[URED_BNBWD_YALL ? j : 0][i][r];
                     float g, xh;
                     if (d.bwd_res == URED_ACT_RES) {
                         g = dh;
@@ -819,8 +793,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const UredGemmDesc d) {
 // kinds feed the same 32x32x2 sequence. The previous layer's BatchNorm+ReLU prologue is
 // applied to the fragments after the LDS read (one fma+max per operand element, hidden
 // under the 64-cycle MFMAs). Two LDS stages, the next K-step's DMA in flight during the
-// current step's MFMAs, one barrier per K-step; blocks loop over output tiles and the
-// next tile's first step is DMA'd during the current tile's epilogue.
+// current step's MFMAs, one barrier per K-step; one output tile per block (two resident per CU).
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 // 1024 16-B chunks per 128x32 operand image; wave w issues chunks [w*256, w*256+256) as 4
@@ -832,16 +805,8 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // k >= K row of a k-major operand: the hardware returns zeros for them.
 constexpr unsigned BUF_OOB = 0x80000000u;
 constexpr int PRO_LDS = 1024;            // max prologue channels staged in LDS by gemm2
-// Persistent tile loop (next tile's first DMA under the current epilogue). Measured neutral
-// on MI355X once the epilogue stops waiting for its stores (lds_barrier), and it costs
-// SGPR spills (every epilogue argument stays live across the main loop), so it is compiled
-// out; kept for experiments.
-constexpr bool GEMM_PERSIST = false;
 #ifndef URED_DMA_SPREAD
 #define URED_DMA_SPREAD 1
-#endif
-#ifndef URED_PRO_PACKED
-#define URED_PRO_PACKED 0
 #endif
 constexpr int BUF_DWORD3 = 0x00020000;   // raw buffer, gfx9 family (gfx950)
 
@@ -922,11 +887,7 @@ __device__ __forceinline__ void dma4(const i32x4& rsrc, unsigned v0, unsigned v1
 // lds: wave-uniform LDS byte address of this wave's first chunk of the operand image
 template <bool KM>
 __device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, unsigned lds) {
-#ifdef URED_DMA_FIXED   // timing experiment only: every K-step re-reads the first K-tile (wrong results)
-    const unsigned toff = 0u * (unsigned)k0 * (unsigned)ld;
-#else
     const unsigned toff = KM ? (unsigned)k0 * (unsigned)ld * 4u : (unsigned)k0 * 4u;
-#endif
     dma4(o.rsrc, o.vo[0] + toff, o.vo[1] + toff, o.vo[2] + toff, o.vo[3] + toff, lds);
 }
 
@@ -962,29 +923,24 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
     const int h = lane >> 5, li = lane & 31;
 
-    // Persistent over output tiles when the grid is smaller than the tile count (launch()
-    // sizes it to the resident-block slots): tile v -> xcd_remap(v), v += gridDim.x.
-    int v = blockIdx.x;
-    if (v >= ntiles) return;
-    auto tile_origin = [&](int vv, int& m0_, int& n0_) {
-        const int tl = xcd_remap(vv, ntiles);
-        m0_ = (tl / ntn) * BM;
-        n0_ = (tl % ntn) * BN;
-    };
+    // one output tile per block: tile blockIdx.x -> xcd_remap (blocks sharing an A panel on one XCD)
+    if ((int)blockIdx.x >= ntiles) return;
     int m0, n0;
-    tile_origin(v, m0, n0);
+    {
+        const int tl = xcd_remap(blockIdx.x, ntiles);
+        m0 = (tl / ntn) * BM;
+        n0 = (tl % ntn) * BN;
+    }
 
     // Operands reach LDS by buffer-descriptor DMA (launch() guarantees buf_ok): a
     // concatenated second A source [M][K-k1] (k1 % BK == 0) gets its own descriptor, chosen
     // per K-step.
     const bool has_a2 = !A_KM && d.k1 < d.K;
     BufOperand ba, ba2, bb;
-    auto setup = [&](int m0_, int n0_) {
-        // a k-major operand's rows past kend must read as zero too (split-K: kend < K)
-        buf_setup<A_KM>(ba, d.A, d.lda, d.M, m0_, A_KM ? kend : min(kend, d.k1), w, lane);
-        if (!A_KM && has_a2) buf_setup<false>(ba2, d.A2, d.lda2, d.M, m0_, d.K - d.k1, w, lane);
-        buf_setup<B_KM>(bb, d.B, d.ldb, d.N, n0_, kend, w, lane);
-    };
+    // a k-major operand's rows past kend must read as zero too (split-K: kend < K)
+    buf_setup<A_KM>(ba, d.A, d.lda, d.M, m0, A_KM ? kend : min(kend, d.k1), w, lane);
+    if (!A_KM && has_a2) buf_setup<false>(ba2, d.A2, d.lda2, d.M, m0, d.K - d.k1, w, lane);
+    buf_setup<B_KM>(bb, d.B, d.ldb, d.N, n0, kend, w, lane);
     // this wave's chunk base in the LDS images, as a wave-uniform byte address (SGPR)
     const unsigned lds_w = __builtin_amdgcn_readfirstlane(
         (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem + (unsigned)w * 4096u);
@@ -996,214 +952,151 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     auto issue_b = [&](int stage, int k0) {
         buf_tile<B_KM>(bb, d.ldb, k0, lds_w + (unsigned)stage * (2u * TILE * 4u) + TILE * 4u);
     };
-    auto issue = [&](int stage, int k0, int, int) { issue_a(stage, k0); issue_b(stage, k0); };
 
     if constexpr (PRO_IN_LDS) {   // visible after the first loop barrier
         for (int i = t; i < d.k1; i += NT) { pro_lds[i] = d.pro_s[i]; pro_lds[PRO_LDS + i] = d.pro_t[i]; }
     }
-    const bool has_k = kbeg < kend;
-    bool after_epi = false;
     int stage = 0;
-    setup(m0, n0);
-    if (has_k) issue(0, kbeg, m0, n0);
+    if (kbeg < kend) { issue_a(0, kbeg); issue_b(0, kbeg); }
 
-    // BN-backward epilogue input Yp by LDS-DMA (URED_YP_LDS): tile row 64hh + 2(8w + q) + (lane>>5),
-    // columns 4(lane&31) .. +3, into stage buffer st at byte (8w + q) KB + 16 lane (row-major,
-    // 128 floats per row). Rows past M read as zeros (descriptor bound); never stored.
-    constexpr bool YPL = URED_YP_LDS && EPI == URED_EPI_BNBWD && !GEMM_PERSIST;
-    i32x4 yrs = {0, 0, 0, 0};
-    unsigned yvo = 0;
-    const unsigned smem_b = __builtin_amdgcn_readfirstlane(
-        (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem);
-    if constexpr (YPL) {
-        yrs = make_rsrc(d.Yp, ((long long)(d.M - 1) * d.ldy + d.N) * 4);
-        yvo = (unsigned)(((long long)(m0 + h) * d.ldy + n0 + 4 * li) * 4);
+    f16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // k-major B with prologue (wgrad): the channel is this lane's output column, fixed
+    float bs_[2] = {1.f, 1.f}, bt_[2] = {0.f, 0.f};
+    if (PRO_B != URED_PRO_NONE) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            int c = n0 + wn * 64 + j * 32 + li;
+            c = c < d.N ? c : d.N - 1;
+            bs_[j] = d.pro_s[c]; bt_[j] = d.pro_t[c];
+        }
+        // Re-define the loaded values through an asm so the compiler's wait for these loads
+        // sits here, once, and not inside the K-loop, where the hardware counter also holds
+        // the (compiler-invisible) next-step DMA and a vmcnt(0) would expose it every step.
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(bs_[0]), "+v"(bs_[1]), "+v"(bt_[0]), "+v"(bt_[1]));
     }
-    auto yp_dma = [&](int hh, int st) {
-        const unsigned ld8 = (unsigned)d.ldy * 8u;            // two rows per DMA instruction
-        const unsigned b = yvo + (unsigned)(hh * 64 + w * 16) * (unsigned)d.ldy * 4u;
-        const unsigned l = __builtin_amdgcn_readfirstlane(smem_b + (unsigned)st * (2u * TILE * 4u) + (unsigned)w * 8192u);
-        dma4(yrs, b, b + ld8, b + 2u * ld8, b + 3u * ld8, l);
-        dma4(yrs, b + 4u * ld8, b + 5u * ld8, b + 6u * ld8, b + 7u * ld8, l + 4096u);
-    };
 
-    while (true) {
-        f16v acc[2][2];
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+        // this wave's share of the step's DMA must have landed before the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        const float* As = smem + stage * 2 * TILE;
+        const float* Bs = As + TILE;
+        const bool tail = k0 + BK > kend;
+        // next step's DMA goes into the other stage (its last readers passed the barrier
+        // above). URED_DMA_SPREAD: its two 4-piece halves are issued between MFMA groups
+        // instead of in one burst in front of the fragment reads (an LDS-DMA piece costs its
+        // wave ~60 cycles among MFMAs, 100-185 beside the step's ds_reads; measured on the
+        // bare loop: 139 -> 146 TF/s, tools/mfma_clock.hip)
+        const bool next = k0 + BK < kend;
+        if (!URED_DMA_SPREAD && next) { issue_a(stage ^ 1, k0 + BK); issue_b(stage ^ 1, k0 + BK); }
+
+        // the prologue's scale/shift first: LDS reads complete in issue order, so the
+        // prologue (and the MFMAs behind it) can start on the first A fragments
+        float ss[16], tt[16];
+        // k1 (start of the raw concatenated A2) is a multiple of BK when A2 is present
+        // (buf_ok), so "this K-step needs the prologue" is wave-uniform: a scalar branch
+        // instead of a per-element select
+        const bool pro_step = PRO_IN_LDS && k0 < d.k1;
+        if (pro_step) {
+            const int kc = min(k0 + 16 * h, d.k1 - 16);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 sv = *reinterpret_cast<const float4*>(pro_lds + kc + 4 * q);
+                const float4 tv = *reinterpret_cast<const float4*>(pro_lds + PRO_LDS + kc + 4 * q);
+                ss[4 * q] = sv.x; ss[4 * q + 1] = sv.y; ss[4 * q + 2] = sv.z; ss[4 * q + 3] = sv.w;
+                tt[4 * q] = tv.x; tt[4 * q + 1] = tv.y; tt[4 * q + 2] = tv.z; tt[4 * q + 3] = tv.w;
+            }
+        }
+        // ---- fragments LDS -> VGPR: a[tm][j], b[tn][j] for k = k0 + 16h + j
+        float a[2][16], b[2][16];
+        if constexpr (!A_KM) {
+#pragma unroll
+            for (int tm = 0; tm < 2; ++tm) {
+                const int r = wm * 64 + tm * 32 + li;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v4 = *reinterpret_cast<const float4*>(As + r * 32 + 4 * ((4 * h + q) ^ ((r >> 1) & 7)));
+                    a[tm][4 * q] = v4.x; a[tm][4 * q + 1] = v4.y; a[tm][4 * q + 2] = v4.z; a[tm][4 * q + 3] = v4.w;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) a[tm][j] = As[(16 * h + j) * BM + wm * 64 + tm * 32 + li];
+        }
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+            const int cidx = wn * 64 + tn * 32 + li;
+            if constexpr (!B_KM) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v4 = *reinterpret_cast<const float4*>(Bs + cidx * 32 + 4 * ((4 * h + q) ^ ((cidx >> 1) & 7)));
+                    b[tn][4 * q] = v4.x; b[tn][4 * q + 1] = v4.y; b[tn][4 * q + 2] = v4.z; b[tn][4 * q + 3] = v4.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) b[tn][j] = Bs[(16 * h + j) * BN + cidx];
+            }
+        }
+
+        // ---- prologues (previous layer's BN+ReLU) and the K tail, on the fragments
+        if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
+            if (pro_step) {
+                // scalar v_fma_f32 + v_max_f32: beside MFMAs a packed v_pk_fma_f32 costs more
+                // issue time than two plain fmas (MI355X_MICROARCH.md, filler prices)
+#pragma unroll
+                for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) a[tm][j] = pro_v<PRO_A>(a[tm][j], ss[j], tt[j]);
+            }
+        }
+        if constexpr (B_KM && PRO_B != URED_PRO_NONE) {
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) b[tn][j] = pro_v<PRO_B>(b[tn][j], bs_[tn], bt_[tn]);
+        }
+        if (tail) {   // zero the k >= K part of the reduction (the images hold clamped copies)
+#pragma unroll
+            for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) a[tm][j] = (k0 + 16 * h + j < kend) ? a[tm][j] : 0.f;
+        }
+        // ---- MFMAs
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[0][j], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[1][j], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[0][j], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][j], acc[1][1], 0, 0, 0);
+            if (URED_DMA_SPREAD && next && j == 1) issue_a(stage ^ 1, k0 + BK);
+            if (URED_DMA_SPREAD && next && j == 5) issue_b(stage ^ 1, k0 + BK);
+        }
+        stage ^= 1;
+    }
+
+#ifdef URED_EXP_NOEPI   // timing experiment only (wrong results): the tile's sum, one store per lane
+    {
+        float sacc = 0.f;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-        // k-major B with prologue (wgrad): the channel is this lane's output column, fixed
-        float bs_[2] = {1.f, 1.f}, bt_[2] = {0.f, 0.f};
-        if (PRO_B != URED_PRO_NONE) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                int c = n0 + wn * 64 + j * 32 + li;
-                c = c < d.N ? c : d.N - 1;
-                bs_[j] = d.pro_s[c]; bt_[j] = d.pro_t[c];
-            }
-            // Re-define the loaded values through an asm so the compiler's wait for these loads
-            // sits here, once, and not inside the K-loop, where the hardware counter also holds
-            // the (compiler-invisible) next-step DMA and a vmcnt(0) would expose it every step.
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(bs_[0]), "+v"(bs_[1]), "+v"(bt_[0]), "+v"(bt_[1]));
-        }
-
-        for (int k0 = kbeg; k0 < kend; k0 += BK) {
-            // This wave's share of the step's DMA must have landed before the barrier. After an
-            // epilogue, the 64 output stores it issued after the prefetch DMA (OutTile) may still
-            // be draining: vmcnt counts in order on gfx9, so <= 63 outstanding covers the DMA.
-            if (k0 == kbeg && after_epi) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_barrier();
-            const float* As = smem + stage * 2 * TILE;
-            const float* Bs = As + TILE;
-            const bool tail = k0 + BK > kend;
-            // next step's DMA goes into the other stage (its last readers passed the barrier
-            // above). URED_DMA_SPREAD: its two 4-piece halves are issued between MFMA groups
-            // instead of in one burst in front of the fragment reads (an LDS-DMA piece costs its
-            // wave ~60 cycles among MFMAs, 100-185 beside the step's ds_reads; measured on the
-            // bare loop: 139 -> 146 TF/s, tools/mfma_clock.hip)
-            const bool next = k0 + BK < kend;
-            if (!URED_DMA_SPREAD && next) issue(stage ^ 1, k0 + BK, m0, n0);
-
-            // the prologue's scale/shift first: LDS reads complete in issue order, so the
-            // prologue (and the MFMAs behind it) can start on the first A fragments
-            float ss[16], tt[16];
-            // k1 (start of the raw concatenated A2) is a multiple of BK when A2 is present
-            // (buf_ok), so "this K-step needs the prologue" is wave-uniform: a scalar branch
-            // instead of a per-element select
-            const bool pro_step = PRO_IN_LDS && k0 < d.k1;
-            if (pro_step) {
-                const int kc = min(k0 + 16 * h, d.k1 - 16);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 sv = *reinterpret_cast<const float4*>(pro_lds + kc + 4 * q);
-                    const float4 tv = *reinterpret_cast<const float4*>(pro_lds + PRO_LDS + kc + 4 * q);
-                    ss[4 * q] = sv.x; ss[4 * q + 1] = sv.y; ss[4 * q + 2] = sv.z; ss[4 * q + 3] = sv.w;
-                    tt[4 * q] = tv.x; tt[4 * q + 1] = tv.y; tt[4 * q + 2] = tv.z; tt[4 * q + 3] = tv.w;
-                }
-            }
-            // ---- fragments LDS -> VGPR: a[tm][j], b[tn][j] for k = k0 + 16h + j
-            float a[2][16], b[2][16];
-            if constexpr (!A_KM) {
-#pragma unroll
-                for (int tm = 0; tm < 2; ++tm) {
-                    const int r = wm * 64 + tm * 32 + li;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float4 v4 = *reinterpret_cast<const float4*>(As + r * 32 + 4 * ((4 * h + q) ^ ((r >> 1) & 7)));
-                        a[tm][4 * q] = v4.x; a[tm][4 * q + 1] = v4.y; a[tm][4 * q + 2] = v4.z; a[tm][4 * q + 3] = v4.w;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) a[tm][j] = As[(16 * h + j) * BM + wm * 64 + tm * 32 + li];
-            }
-#pragma unroll
-            for (int tn = 0; tn < 2; ++tn) {
-                const int cidx = wn * 64 + tn * 32 + li;
-                if constexpr (!B_KM) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float4 v4 = *reinterpret_cast<const float4*>(Bs + cidx * 32 + 4 * ((4 * h + q) ^ ((cidx >> 1) & 7)));
-                        b[tn][4 * q] = v4.x; b[tn][4 * q + 1] = v4.y; b[tn][4 * q + 2] = v4.z; b[tn][4 * q + 3] = v4.w;
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) b[tn][j] = Bs[(16 * h + j) * BN + cidx];
-                }
-            }
-
-            // ---- prologues (previous layer's BN+ReLU) and the K tail, on the fragments
-            if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
-                if (pro_step) {
-#if URED_PRO_PACKED
-                    // the two M-halves share channel j: one packed fma (v_pk_fma_f32) per pair
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) {
-                        f2v v = {a[0][j], a[1][j]};
-                        const f2v sv = {ss[j], ss[j]}, tv = {tt[j], tt[j]};
-                        if (PRO_A == URED_PRO_RES) v = (f2v){fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
-                        v = __builtin_elementwise_fma(v, sv, tv);
-                        if (PRO_A == URED_PRO_ENC) v = (f2v){fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
-                        a[0][j] = v.x; a[1][j] = v.y;
-                    }
-#else
-                    // scalar v_fma_f32 + v_max_f32: beside MFMAs a packed v_pk_fma_f32 costs more
-                    // issue time than two plain fmas (MI355X_MICROARCH.md, filler prices)
-#pragma unroll
-                    for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-                        for (int j = 0; j < 16; ++j) a[tm][j] = pro_v<PRO_A>(a[tm][j], ss[j], tt[j]);
-#endif
-                }
-            }
-            if constexpr (B_KM && PRO_B != URED_PRO_NONE) {
-#pragma unroll
-                for (int tn = 0; tn < 2; ++tn)
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) b[tn][j] = pro_v<PRO_B>(b[tn][j], bs_[tn], bt_[tn]);
-            }
-            if (tail) {   // zero the k >= K part of the reduction (the images hold clamped copies)
-#pragma unroll
-                for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) a[tm][j] = (k0 + 16 * h + j < kend) ? a[tm][j] : 0.f;
-            }
-            // ---- MFMAs
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[0][j], acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[1][j], acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[0][j], acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][j], acc[1][1], 0, 0, 0);
-                if (URED_DMA_SPREAD && next && j == 1) issue_a(stage ^ 1, k0 + BK);
-                if (URED_DMA_SPREAD && next && j == 5) issue_b(stage ^ 1, k0 + BK);
-                if (YPL && !next && j == 1) yp_dma(0, stage ^ 1);
-                if (YPL && !next && j == 8) {     // every wave has its fragments: `stage` is free
-                    lds_barrier();
-                    yp_dma(1, stage);
-                }
-            }
-            stage ^= 1;
-        }
-
-        // The stage `stage` was last read one K-step ago (a barrier has passed since), so the
-        // next tile's first step can be DMA'd into it while this tile's epilogue runs.
-        const int nv = v + gridDim.x;
-        int nm0 = 0, nn0 = 0;
-        if (GEMM_PERSIST && nv < ntiles) tile_origin(nv, nm0, nn0);
-        auto pre = [&]() {
-            if (GEMM_PERSIST && nv < ntiles) {
-                setup(nm0, nn0);
-                if (has_k) issue(stage, kbeg, nm0, nn0);
-            }
-        };
-        if (YPL && !has_k) { yp_dma(0, stage); yp_dma(1, stage ^ 1); }
-#ifdef URED_EXP_NOEPI   // timing experiment only (wrong results): the tile's sum, one store per lane
-        {
-            float sacc = 0.f;
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) sacc += acc[i][j][r];
-            if (sacc == 1234.5f) d.C[t] = sacc;
-        }
-#else
-        epilogue<EPI, true, YPL>(d, acc, m0, n0, red_f, red_i, pre, smem + stage * 2 * TILE,
-                                 smem + (stage ^ 1) * 2 * TILE);
-#endif
-        if (!GEMM_PERSIST || nv >= ntiles) break;
-        v = nv; m0 = nm0; n0 = nn0;
-        after_epi = true;
+                for (int r = 0; r < 16; ++r) sacc += acc[i][j][r];
+        if (sacc == 1234.5f) d.C[t] = sacc;
     }
+#else
+    epilogue<EPI, true>(d, acc, m0, n0, red_f, red_i);
+#endif
 }
 
 // ---- small kernels -------------------------------------------------------------
@@ -1669,24 +1562,6 @@ bool v2_ok(const UredGemmDesc& d) {
     return true;
 }
 
-// Resident-block slots of the current device for the persistent v2 kernel (2 blocks of 256
-// threads per CU: VGPR-bound), a multiple of 8 so that blockIdx % 8 stays the XCD.
-// URED_GEMM_PERSIST=0 launches one block per tile instead.
-int persist_slots() {
-    static const bool on = [] { const char* e = getenv("URED_GEMM_PERSIST"); return !(e && e[0] == '0'); }();
-    if (!on) return 0;
-    thread_local int dev_cached = -1, slots = 0;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    if (dev != dev_cached) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
-        slots = (2 * cus) / 8 * 8;
-        dev_cached = dev;
-    }
-    return slots;
-}
-
 // 256 threads per 128-row block (1024 measured no faster and changes the summation order)
 constexpr int SMALL_NT = 256;
 
@@ -1848,11 +1723,8 @@ void launch(const UredGemmDesc& d, hipStream_t st) {
     if (EPI == URED_EPI_FWD && fwd_small_ok(d)) { launch_fwd_small(d, st); return; }
     const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
     dim3 grid(ntm * ntn, 1, EPI == URED_EPI_SPLITK ? d.splits : 1);
-    if (vec_ok(d) && v2_ok(d) && buf_ok(d)) {
-        const int slots = (EPI == URED_EPI_SPLITK || !GEMM_PERSIST) ? 0 : persist_slots();
-        if (slots > 0 && (int)grid.x > slots) grid.x = slots;
+    if (vec_ok(d) && v2_ok(d) && buf_ok(d))
         hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI>), grid, dim3(NT), 0, st, d);
-    }
     else if (vec_ok(d)) hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, true>), grid, dim3(NT), 0, st, d);
     else hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, false>), grid, dim3(NT), 0, st, d);
 }

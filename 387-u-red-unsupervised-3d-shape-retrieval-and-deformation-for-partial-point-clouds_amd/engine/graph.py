@@ -133,7 +133,11 @@ class GraphedStep:
             return _detached(T)
         self._fresh_grads()
         loss, T = self.inner.forward(batch, epoch)
-        self.inner.begin_backward()
+        if self._inline():
+            # the same bucketed all-reduces as a replay of the captured graph issues; with gloo the
+            # replay reduces after the backward, and so does this step (ranks can miss a graph at
+            # different steps: their collective sequences must still match)
+            self.inner.begin_backward()
         loss.backward()
         del loss
         self.inner.reduce_gradients()

@@ -86,6 +86,11 @@ def _worker(rank, world, port, bs, npts, q):
                 # bound of a fp32 sum of `world` terms is relative to the sum of magnitudes
                 mag = sum(a.abs() for a in allg) / world
                 err = float(((p.grad - mean).abs() / (mag + 1e-30)).max())
+                if err > worst:
+                    name = next(f"{m}.{k}" for m in step.models for k, q in step.models[m].named_parameters() if q is p)
+                    i = int(((p.grad - mean).abs() / (mag + 1e-30)).argmax())
+                    res["worst_at"] = (it, name, i, float(p.grad.reshape(-1)[i]), float(mean.reshape(-1)[i]),
+                                       float(mag.reshape(-1)[i]), [float(a_.reshape(-1)[i]) for a_ in allg])
                 worst = max(worst, err)
                 ok_avg &= err <= 1e-5
             step.clip_and_step()
@@ -120,7 +125,7 @@ def _run(world, bs, npts):
         p.join(timeout=60)
     for r in res:
         assert "error" not in r, r
-        assert r["avg"], r
+        assert r["avg"], (r["rank"], r["worst_rel_err"], r.get("worst_at"), r)
         assert r["same_params"], r
         assert all(math.isfinite(v) for v in r["losses"]), r
     first = sorted(r["losses"][0] for r in res)

@@ -266,3 +266,34 @@ def test_wgrad_skinny_edge_layers(K, dev, Cout, Kin, pro, M):
     acc = prev.to(dev)
     K.wgrad(dY.to(dev), ldd, X.to(dev), ldx, Cout, Kin, M, acc, Kin, X_off=xoff, accumulate=True, **kw)
     close(acc, ref + prev.double(), 1e-5, "wgrad skinny accumulate")
+
+
+@pytest.mark.parametrize("M,N,Kd", [(32768, 1024, 1024), (8192, 512, 512), (4096, 256, 1152)])
+def test_gemm_fp32_accuracy_vs_float64(dev, M, N, Kd):
+    """The MLP GEMMs (v_mfma_f32_32x32x2_f32, csrc/mlp.hip gemm2_kernel) against float64 matmuls
+    of the same fp32 inputs at step-like shapes: forward with the BN+ReLU prologue, dgrad with a
+    k-major weight and split-K wgrad within 4e-6 of max |y| (measured 1.1e-6 to 1.6e-6,
+    tools/emu_accuracy.py), and bitwise equal from run to run."""
+    from ured_hip import kernels as K
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    X = torch.randn(M, Kd, device=dev, generator=g)
+    W = torch.randn(N, Kd, device=dev, generator=g) * Kd ** -0.5
+    s = torch.rand(Kd, device=dev, generator=g) + 0.5
+    t = torch.randn(Kd, device=dev, generator=g) * 0.1
+    Y = torch.empty(M, N, device=dev)
+    K.gemm(M, N, Kd, X, Kd, W, Kd, Y, N, pro_a=K.PRO_ENC, pro_s=s, pro_t=t)
+    dY = torch.randn(M, N, device=dev, generator=g)
+    G = torch.empty(M, Kd, device=dev)
+    K.gemm(M, Kd, N, dY, N, W, Kd, G, Kd, b_kmajor=True)
+    dW = torch.empty(N, Kd, device=dev)
+    K.wgrad(dY, N, X, Kd, N, Kd, M, dW, Kd)
+    refs = {"fwd": (Y, torch.relu(X.double() * s.double() + t.double()) @ W.double().t()),
+            "dgrad": (G, dY.double() @ W.double()), "wgrad": (dW, dY.double().t() @ X.double())}
+    for name, (y, r) in refs.items():
+        e = float((y.double() - r).abs().max() / r.abs().max())
+        assert e <= 4e-6, (name, e)
+    Y2, G2, dW2 = torch.empty_like(Y), torch.empty_like(G), torch.empty_like(dW)     # run to run: bitwise
+    K.gemm(M, N, Kd, X, Kd, W, Kd, Y2, N, pro_a=K.PRO_ENC, pro_s=s, pro_t=t)
+    K.gemm(M, Kd, N, dY, N, W, Kd, G2, Kd, b_kmajor=True)
+    K.wgrad(dY, N, X, Kd, N, Kd, M, dW2, Kd)
+    assert torch.equal(Y, Y2) and torch.equal(G, G2) and torch.equal(dW, dW2)
