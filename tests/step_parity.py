@@ -32,6 +32,17 @@ ENC_BN_FED = ("mlp1.0.bias", "mlp1.3.bias", "mlp2.0.bias", "mlp2.3.bias", "mlp2.
 ENCODERS = ("src_encoder_all", "target_encoder_full")
 
 
+class ParityReport(UserWarning):
+    """Carries the parity tests' measured numbers (tie gaps, loss-term deviations, worst gradient
+    tensors) into pytest's warnings summary, so a quiet (-q) run still shows them."""
+
+
+def report(line):
+    import warnings
+    print(line)
+    warnings.warn(line.strip(), ParityReport, stacklevel=2)
+
+
 def record_pools(models, on=True):
     for name in ENCODERS:
         models[name].record_pool = on
@@ -89,7 +100,7 @@ def tie_report(pool_rec, label=""):
     for k, st in sorted(ured_ref.NN_TIE_STATS.items()):
         parts.append(f"NN {k}: {st['overridden']} overridden ({st['exact_ties']} exact, {st['near_ties']} near), "
                      f"max {st['max_over_bound']:.2f} of the bound")
-    print(f"\n{label} ties: " + "; ".join(parts))
+    report(f"\n{label} ties: " + "; ".join(parts))
 
 
 def same_pools(choices, oracle_pool):
@@ -107,7 +118,7 @@ def check_loss_terms(got, ref, label=""):
     """got/ref: {term: float}. Prints every term's relative deviation; asserts LOSS_RTOL."""
     assert set(got) == set(ref), (sorted(got), sorted(ref))
     dev = {k: abs(got[k] - ref[k]) / max(abs(ref[k]), 1e-30) for k in ref}
-    print(f"\n{label} loss-term rel dev: " + ", ".join(f"{k} {v:.1e}" for k, v in sorted(dev.items())))
+    report(f"\n{label} loss-term rel dev: " + ", ".join(f"{k} {v:.1e}" for k, v in sorted(dev.items())))
     for k, v in dev.items():
         assert v <= LOSS_RTOL, f"{label} {k}: {got[k]!r} vs {ref[k]!r} (rel {v:.2e} > {LOSS_RTOL})"
     return dev
@@ -148,7 +159,7 @@ def check_grads(models, ref_grads, label="", ref32=None, grad_rel=GRAD_REL, grad
             nbig += int(((g - r).abs() > 2e-3 * r.abs().max()).sum())
             n += 1
     rows.sort(key=lambda t: -t[0])
-    print(f"{label} {n} gradient tensors ({floored} with an fp32 floor above {grad_rel:g}/{grad_elem:g}; "
+    report(f"{label} {n} gradient tensors ({floored} with an fp32 floor above {grad_rel:g}/{grad_elem:g}; "
           f"{nbig} elements off by > 2e-3 of their tensor's max); "
           f"worst rel-norm / elementwise dev [fp32 oracle's]: " +
           "; ".join(f"{name} {rel:.1e}/{elem:.1e} [{f[0]:.1e}/{f[1]:.1e}]" for rel, elem, name, f, _, _ in rows[:6]))

@@ -243,7 +243,7 @@ def test_config3_inference_full_size(dev):
     near = (R["sim_top2_gap"] < 1e-6) & valid
     mism = (got != ref) & ~near
     flips = int(((got != ref) & near).sum())
-    print(f"\nconfig3: {int(valid.sum())} retrievals, {int(near.sum())} near-ties (gap < 1e-6), {flips} flipped")
+    step_parity.report(f"\nconfig3: {int(valid.sum())} retrievals, {int(near.sum())} near-ties (gap < 1e-6), {flips} flipped")
     assert int(mism.sum()) == 0, f"{int(mism.sum())} retrieval mismatches outside near-ties"
     same = (got == ref).all(dim=1)
     assert int(same.sum()) >= 12
