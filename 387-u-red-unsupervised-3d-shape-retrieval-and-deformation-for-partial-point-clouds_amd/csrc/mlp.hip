@@ -1083,20 +1083,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         stage ^= 1;
     }
 
-#ifdef URED_EXP_NOEPI   // timing experiment only (wrong results): the tile's sum, one store per lane
-    {
-        float sacc = 0.f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sacc += acc[i][j][r];
-        if (sacc == 1234.5f) d.C[t] = sacc;
-    }
-#else
     epilogue<EPI, true>(d, acc, m0, n0, red_f, red_i);
-#endif
 }
 
 // ---- small kernels -------------------------------------------------------------
@@ -1550,12 +1537,7 @@ bool vec_ok(const UredGemmDesc& d) {
 
 // v2 additionally needs the A prologue channels to come in 16-aligned runs (k1 % 16 == 0) and
 // rows/extents >= 4 so clamped 16-B sources stay in bounds.
-bool v2_enabled() {
-    static const bool on = [] { const char* e = getenv("URED_GEMM_V1"); return !(e && e[0] == '1'); }();
-    return on;
-}
 bool v2_ok(const UredGemmDesc& d) {
-    if (!v2_enabled()) return false;
     if (d.pro_a && (d.k1 % 16 != 0)) return false;
     if (d.pro_a && !d.a_kmajor && d.k1 > PRO_LDS) return false;
     if (d.K < 4 || (d.a_kmajor && d.M < 4) || (d.b_kmajor && d.N < 4)) return false;

@@ -50,6 +50,7 @@ import gc
 import torch
 
 from ured_hip.collective import SegmentedCapture
+from ured_hip.ops import refresh_static
 
 
 def _clone_batch(batch):
@@ -223,8 +224,7 @@ class GraphedStep:
             return T
         self.graphs.move_to_end(k)
         static, cap, T, inline = ent
-        for name, v in static.items():
-            v.copy_(batch[name], non_blocking=True)
+        refresh_static(static, batch)        # one ured_copy_batch launch for the input tensors
         cap.replay()                         # segments, and the collectives between them
         if not inline:
             self.inner.reduce_gradients()

@@ -33,6 +33,7 @@ from dataset.dataset_utils import cal_retrieval_score, deform_vertices, get_shap
 from engine.train import batch_to_device, get_models, get_part  # noqa: E402
 from loss.chamfer_loss import compute_cm_loss  # noqa: E402
 from train_utils.load_sources import load_sources  # noqa: E402
+from ured_hip.ops import refresh_static  # noqa: E402
 
 
 @torch.no_grad()
@@ -130,8 +131,7 @@ class GraphedInfer:
             self.graphs[k] = (static, g, out)
             return r
         static, g, out = ent
-        for n in self.INPUTS:
-            static[n].copy_(batch[n], non_blocking=True)
+        refresh_static(static, {n: batch[n] for n in self.INPUTS})    # one batched copy launch
         g.replay()
         return out
 

@@ -40,7 +40,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 6   /* 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
+#define URED_ABI_VERSION 7   /* 7: ured_copy_batch; 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
@@ -432,6 +432,14 @@ int ured_build_parts(const long long* labels, const float* x, int B, int N, int 
                      long long* perm, long long* inv_perm, int* gid, int* off, long long* counts,
                      long long* k, float* mask, long long* rank_of_label, unsigned char* present,
                      float* aabb, float* param_def, void* stream);
+
+/* Several device-to-device copies in one launch (csrc/copy.hip): the HIP-graph step refreshes its
+ * static input batch before each replay (engine/graph.py) with this instead of one blit per
+ * tensor. dst[i][0, bytes[i]) = src[i][0, bytes[i]); regions must not overlap; 16-B moves where
+ * both addresses and the size allow, else 4-B or 1-B moves for that item. */
+#define URED_COPY_MAX 16
+typedef struct { void* dst; const void* src; long long bytes; } UredCopyItem;
+int ured_copy_batch(const UredCopyItem* items, int n, void* stream);
 
 /* ---------------- loss head (csrc/loss.hip) ---------------- */
 /* compute_cm_loss of the deformed shape `out` [B,S,3] and of its mirror image (x -> -x,

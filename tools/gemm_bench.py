@@ -30,6 +30,7 @@ STEP_SHAPES = [  # config-2 step sizes (unique-source encoding: M = 32768 target
     ("step tgt.ppo3 512->512", 32768, 512, 512),
     ("step tgt.mlp 128->1024", 32768, 1024, 128),
     ("step R1 512->256", 32768, 256, 512),
+    ("step R3 256->32", 32768, 32, 256),
 ]
 
 
