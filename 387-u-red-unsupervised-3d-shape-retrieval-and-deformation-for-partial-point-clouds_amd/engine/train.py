@@ -96,16 +96,18 @@ class ReInput:
         self.pp_sorted, self.part_mean, self.gid, self.off = pp_sorted, part_mean, gid, off
 
 
-def get_part(cfg, per_point_full, target_labels, x):
+def get_part(cfg, per_point_full, target_labels, x, alias=False):
     """engine/train.py:103-136 without host syncs. per_point_full [B, N, C].
 
     Returns (target_part_f [B,P,C], None (the unused per-part feature lists), ReInput,
-    mask_part [B,P], PartBatch (the part_x lists), param_def [B,P,6]).
+    mask_part [B,P], PartBatch (the part_x lists), param_def [B,P,6]); alias=True appends
+    per_point_full as an output of the regrouping (ured_hip.ops.PartRowsFn) for another consumer,
+    whose gradient is then added inside the regrouping's backward pass.
     """
     B, N, C = per_point_full.shape
     P = cfg["MAX_NUM_PARTS"]
     parts = build_parts(target_labels, x, P)
-    pp_sorted, sums = part_rows(per_point_full, parts)
+    pp_sorted, sums, *pp_alias = part_rows(per_point_full, parts, alias=alias)
     part_mean = sums / parts.counts.reshape(-1, 1).clamp(min=1).float()
     param_def = getattr(parts, "param_def", None)                      # indexed by label value (train.py:120)
     if param_def is None:
@@ -113,7 +115,7 @@ def get_part(cfg, per_point_full, target_labels, x):
         param_def = torch.gather(aabb, 1, parts.rank_of_label.clamp(min=0).unsqueeze(-1).expand(-1, -1, 6))
         param_def = param_def * parts.present.unsqueeze(-1).float()
     return (part_mean.view(B, P, C), None, ReInput(pp_sorted, part_mean, parts.gid, parts.off),
-            parts.mask, parts, param_def)
+            parts.mask, parts, param_def) + tuple(pp_alias)
 
 
 class TrainStep:
@@ -239,11 +241,16 @@ class TrainStep:
         src_points = get_source_points(src_labels, self.db) if uq is None else None
         codes, rec_u, pts_u, inv = self._source_branch(uq, src_points, src_sem_f, B, P, expand_rec=False)
         tcode, pp = M["target_encoder_full"].forward_pointmajor(x, tgt_sem_f)
-        target_part_f, _, re_in, mask_part, parts, param_def = get_part(cfg, pp.view(B, N, -1), batch["labels"], x)
+        # the per-point features feed get_part's regrouping and the reconstruction decoder: the
+        # decoder reads them through the regrouping's alias output, so their two gradients are
+        # summed in the regrouping's backward pass
+        target_part_f, _, re_in, mask_part, parts, param_def, pp_alias = get_part(cfg, pp.view(B, N, -1),
+                                                                                 batch["labels"], x, alias=True)
         codes = codes.view(B, P, -1)
         params_full = M["param_decoder_full"](tcode, codes, None)
         out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
-        recon_full_p = M["recon_decoder_full"].forward_split(pp, tcode, group_rows=N).view(B, N, 3)
+        recon_full_p = M["recon_decoder_full"].forward_split(pp_alias.view(B * N, -1), tcode,
+                                                             group_rows=N).view(B, N, 3)
         re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
                                                          off=re_in.off).view(B, N, 3)
         param = regularization_param(params_full, mask_part) if cfg.get("use_param_loss", 0.0) > 0.0 else None

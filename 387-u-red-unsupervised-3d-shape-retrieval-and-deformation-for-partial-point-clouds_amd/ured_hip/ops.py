@@ -81,10 +81,15 @@ class PartRowsFn(Function):
     """get_part's regrouping of per-point features (engine/train.py:103-136): x [B, N, C] ->
     (rows sorted by part label [B*N, C], per-part-slot sums [G, C]). Forward: one gather and one
     HIP segment sum; backward: ONE HIP pass (ured_part_rows_bwd) where the separate ops would
-    take an index_select of the part gradients, an add and the inverse-permutation gather."""
+    take an index_select of the part gradients, an add and the inverse-permutation gather.
+
+    alias=True adds a third output: x itself, for a second consumer of the features (the
+    reconstruction decoder, engine/train.py:240,250). Its gradient then arrives in this backward
+    beside the regrouping's and is added inside the same pass (ured_part_rows_bwd_add) instead of
+    in a separate autograd add over the whole [B, N, C] tensor."""
 
     @staticmethod
-    def forward(ctx, x, perm, inv, off, gid):
+    def forward(ctx, x, perm, inv, off, gid, alias=False):
         B, N, C = x.shape
         x = x.contiguous()
         if perm.dtype != torch.int64 or gid.dtype != torch.int32:
@@ -98,26 +103,28 @@ class PartRowsFn(Function):
         sums = K.group_colsum(xs, C, off.shape[0] - 1, off=off)
         ctx.save_for_backward(inv, gid)
         ctx.shape = (B, N, C)
-        return xs, sums
+        return (xs, sums, x) if alias else (xs, sums)
 
     @staticmethod
-    def backward(ctx, d_sorted, d_sums):
+    def backward(ctx, d_sorted, d_sums, d_x=None):
         inv, gid = ctx.saved_tensors
         B, N, C = ctx.shape
         ds = None if d_sorted is None else d_sorted.contiguous()
         dg = None if d_sums is None else d_sums.contiguous()
+        dx = None if d_x is None else d_x.contiguous()
         if inv.dtype != torch.int64 or gid.dtype != torch.int32:
             raise TypeError("part_rows: inv must be int64 and gid int32")
         out = torch.empty(B, N, C, device=inv.device)
-        _lib.call("ured_part_rows_bwd", _lib.ptr(ds), _lib.ptr(dg), _lib.ptr(inv.contiguous()),
-                  _lib.ptr(gid.contiguous()), B, N, C, _lib.ptr(out), _lib.stream_of(out))
-        return out, None, None, None, None
+        _lib.call("ured_part_rows_bwd_add", _lib.ptr(ds), _lib.ptr(dg), _lib.ptr(inv.contiguous()),
+                  _lib.ptr(gid.contiguous()), B, N, C, _lib.ptr(dx), _lib.ptr(out), _lib.stream_of(out))
+        return out, None, None, None, None, None
 
 
-def part_rows(x, parts):
-    """(x regrouped by part [B*N, C], per-part-slot sums [B*P, C]) for a PartBatch."""
+def part_rows(x, parts, alias=False):
+    """(x regrouped by part [B*N, C], per-part-slot sums [B*P, C]) for a PartBatch; alias=True
+    also returns x itself as a third output whose gradient PartRowsFn adds in its own pass."""
     _lib.require_device(x)
-    return PartRowsFn.apply(x, parts.perm, parts.inv_perm, parts.off, parts.gid)
+    return PartRowsFn.apply(x, parts.perm, parts.inv_perm, parts.off, parts.gid, alias)
 
 
 def segment_sum(x, off, gid):

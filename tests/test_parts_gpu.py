@@ -90,6 +90,35 @@ def test_part_rows_matches_separate_ops(dev, B, N, P, C, kmax):
         assert torch.equal(a.grad, b.grad), (a.grad - b.grad).abs().max().item()
 
 
+@pytest.mark.parametrize("B,N,P,C,kmax", [(16, 2048, 16, 512, 4), (3, 700, 16, 6, 16)])
+def test_part_rows_alias_gradient(dev, B, N, P, C, kmax):
+    """part_rows(alias=True): the third output is x itself (same values, same storage) and the
+    gradient reaching it is added inside the regrouping's backward pass — equal, bitwise, to
+    autograd's own sum when the second consumer reads x directly."""
+    from ured_hip.ops import build_parts, part_rows
+    g = torch.Generator().manual_seed(B + N + C)
+    x = torch.randn(B, N, C, generator=g).to(dev)
+    labels = torch.randint(0, kmax, (B, N), generator=g).to(dev)
+    parts = build_parts(labels, torch.randn(B, N, 3, generator=g).to(dev), P)
+    gs, gp = torch.randn(B * N, C, generator=g).to(dev), torch.randn(B * P, C, generator=g).to(dev)
+    gx = torch.randn(B, N, C, generator=g).to(dev)
+    a = x.clone().requires_grad_(True)
+    xs, sums, xa = part_rows(a, parts, alias=True)
+    assert xa.data_ptr() == a.data_ptr() and torch.equal(xa, a)
+    torch.autograd.backward([xs, sums, xa * 1.0], [gs, gp, gx])
+    b = x.clone().requires_grad_(True)
+    xs2, sums2 = part_rows(b, parts)
+    torch.autograd.backward([xs2, sums2, b * 1.0], [gs, gp, gx])
+    assert torch.equal(a.grad, b.grad), (a.grad - b.grad).abs().max().item()
+    c = x.clone().requires_grad_(True)                  # alias output unused: no third gradient
+    xs3, sums3, _ = part_rows(c, parts, alias=True)
+    torch.autograd.backward([xs3, sums3], [gs, gp])
+    d = x.clone().requires_grad_(True)
+    xs4, sums4 = part_rows(d, parts)
+    torch.autograd.backward([xs4, sums4], [gs, gp])
+    assert torch.equal(c.grad, d.grad)
+
+
 @pytest.mark.parametrize("B,N,P,gaps", [(3, 257, 16, True), (16, 2048, 16, False), (2, 5000, 32, True), (1, 7, 16, True)])
 def test_build_parts_kernel_equals_composed(dev, B, N, P, gaps):
     """ured_build_parts (one launch: stable counting sort, slot tables, boxes, param_def) == the
