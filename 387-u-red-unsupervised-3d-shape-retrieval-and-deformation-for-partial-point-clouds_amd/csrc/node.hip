@@ -218,9 +218,14 @@ __global__ __launch_bounds__(NG_NT, URED_NODE_WG_PER_CU * NG_WAVES / 4) void nod
 }
 
 // ---- BatchNorm1d over node sets (rows [off[s], off[s+1]) form one call of the module) -------
-// One workgroup per 16 columns, 16 row lanes per column; sets processed in order, so the
-// running statistics see the reference's sequence of module calls. fp64 sums, fixed order.
-constexpr int BN_COLS = 16, BN_RL = 16, BN_NT = BN_COLS * BN_RL;
+// One workgroup per 4 columns, 64 row lanes per column (a set of <= 288 node rows is a few
+// dependent loads per lane; 16 columns x 16 lanes ran 1.2-1.5x longer, tools/node_bn_bench.py);
+// sets processed in order, so the running statistics see the reference's sequence of module
+// calls. fp64 sums, fixed order.
+#ifndef URED_NODE_BN_COLS
+#define URED_NODE_BN_COLS 4
+#endif
+constexpr int BN_COLS = URED_NODE_BN_COLS, BN_RL = 256 / BN_COLS, BN_NT = BN_COLS * BN_RL;
 
 __device__ __forceinline__ float bn_in(const float* Y, int ldy, int m, int n, int relu_in) {
     const float y = Y[(long long)m * ldy + n];
