@@ -34,9 +34,20 @@ struct AttnArgs {
     float* dv; int lddv;
 };
 
-// Load rows x (row stride ld, head offset h*d) of `rows` nodes into LDS [rows][d+1].
+// Load rows x (row stride ld, head offset h*d) of `rows` nodes into LDS [rows][d+1]: 16-B global
+// loads when the head slice is 16-B aligned (the fused projection outputs are), else 4-B loads.
 __device__ inline void load_rows(float* dst, const float* src, int ld, int rows, int d, int hoff, int b) {
     const int dp = d + 1;
+    if (((d | ld | hoff) & 3) == 0 && ((uintptr_t)src & 15) == 0) {
+        const int d4 = d >> 2;
+        for (int e = threadIdx.x; e < rows * d4; e += ATT_THREADS) {
+            const int r = e / d4, c = (e - r * d4) * 4;
+            const float4 v = *reinterpret_cast<const float4*>(src + (size_t)(b * rows + r) * ld + hoff + c);
+            float* o = dst + r * dp + c;
+            o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+        }
+        return;
+    }
     for (int e = threadIdx.x; e < rows * d; e += ATT_THREADS) {
         const int r = e / d, c = e - r * d;
         dst[r * dp + c] = src[(size_t)(b * rows + r) * ld + hoff + c];
