@@ -64,6 +64,7 @@ _SHAPE_LOG = [] if os.environ.get("URED_GEMM_SHAPES") else None    # diagnostics
 # K slice per split of the few-tile store GEMMs (the per-sample fc layers, M = batch): the
 # per-split K-loop is a chain of dependent DMA round trips, so shorter slices = more workgroups
 _SPLITK_KMIN = 32
+_SPLITK_MIN_K = 256     # split from K = 256 (the decoders' 16/256-row code gradients: 22 -> ~8 us; +0.2 % step)
 
 
 def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro_a=PRO_NONE, pro_b=PRO_NONE,
@@ -74,7 +75,7 @@ def gemm(M, N, K, A, lda, B, ldb, C, ldc, *, a_kmajor=False, b_kmajor=False, pro
     """One ured_gemm launch (two when a plain store GEMM with few output tiles and a long K is
     split over K: split-K partials + a reduce that adds the bias). Offsets are in elements."""
     if (epi == EPI_STORE and pro_a == PRO_NONE and pro_b == PRO_NONE and A2 is None and not a_kmajor
-            and K >= 512):
+            and K >= _SPLITK_MIN_K):
         tiles = ((M + BM - 1) // BM) * ((N + BM - 1) // BM)
         if tiles <= 16:
             sp = min(1024 // tiles, K // _SPLITK_KMIN)
