@@ -19,5 +19,7 @@ cd $R
 python3 tools/trace_stats.py gpurun_out/${T}_trace gpurun_out/${T}_trace_stats.csv --top 60 > gpurun_out/${T}_trace_top.txt
 python3 tools/trace_stats.py gpurun_out/${T}_trace gpurun_out/${T}_trace_timed_stats.csv --tail $K/$((K + 5)) --top 60 > gpurun_out/${T}_trace_timed_top.txt
 python3 tools/trace_stats.py gpurun_out/${T}_stats gpurun_out/${T}_stats_timed_stats.csv --tail $K/$((K + 5)) --top 5 > /dev/null
+# one replayed step's kernel sequence (durations, gaps) for the tail breakdown
+python3 tools/trace_seq.py gpurun_out/${T}_trace > gpurun_out/${T}_seq.txt 2>&1 || true
 find gpurun_out/${T}_stats gpurun_out/${T}_trace -name "*kernel_trace.csv" -delete
 head -30 gpurun_out/${T}_trace_top.txt
