@@ -19,7 +19,8 @@ def main():
     from ured_hip import node
     dev = torch.device("cuda:0")
     for (M, N, K) in [(32, 512, 32), (32, 512, 512), (32, 1024, 1024), (288, 512, 512), (288, 1536, 512),
-                      (256, 1024, 1024), (1024, 1024, 288)]:
+                      (256, 1024, 1024), (288, 1024, 1024), (288, 512, 1024), (1024, 1024, 288), (16, 256, 1024),
+                      (256, 256, 512)]:
         x = torch.randn(M, K, device=dev)
         W = torch.randn(N, K, device=dev)
         y = torch.empty(M, N, device=dev)
