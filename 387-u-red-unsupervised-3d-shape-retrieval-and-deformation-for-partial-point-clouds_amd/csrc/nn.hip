@@ -115,13 +115,41 @@ __global__ __launch_bounds__(NN_THREADS) void nn_fwd_kernel(NNFwdArgs args) {
         // whole chunks (RS * sub <= TILE, since TILE is a multiple of RS * NN_CHUNK)
         const int sub = ALL ? ((tn + RS - 1) / RS + NN_CHUNK - 1) / NN_CHUNK * NN_CHUNK : SUB;
         __syncthreads();
-        for (int i = t; i < (ALL ? RS * sub : TILE); i += NN_THREADS) {
-            float x = NN_PAD, y = NN_PAD, z = NN_PAD;
-            if (i < tn) {
-                const float* p = R + 3 * (size_t)(r_off + t0 + i);
-                x = p[0]; y = p[1]; z = p[2];
+        const int fill = ALL ? RS * sub : TILE;
+        const float* rp = R + 3 * (size_t)(r_off + t0);
+        if ((((uintptr_t)rp) & 15) == 0) {
+            // four points (three float4) per thread and step, the steps unrolled so their loads
+            // are in flight together; SoA rows written as float4
+            const int full = min(tn, fill) >> 2;             // whole groups of 4 points
+            const int part = (tn < fill && (tn & 3)) ? full : -1;   // the group holding the last point
+#pragma unroll 4
+            for (int i4 = t; i4 < (fill >> 2); i4 += NN_THREADS) {
+                if (i4 == part) continue;
+                float4 v0 = make_float4(NN_PAD, NN_PAD, NN_PAD, NN_PAD), v1 = v0, v2 = v0;
+                if (i4 < full) {
+                    const float4* q4 = reinterpret_cast<const float4*>(rp) + 3 * i4;
+                    v0 = q4[0]; v1 = q4[1]; v2 = q4[2];
+                }
+                *reinterpret_cast<float4*>(sx + 4 * i4) = make_float4(v0.x, v0.w, v1.z, v2.y);
+                *reinterpret_cast<float4*>(sy + 4 * i4) = make_float4(v0.y, v1.x, v1.w, v2.z);
+                *reinterpret_cast<float4*>(sz + 4 * i4) = make_float4(v0.z, v1.y, v2.x, v2.w);
             }
-            sx[i] = x; sy[i] = y; sz[i] = z;
+            // the partial group, point by point
+            if (part >= 0 && t < 4) {
+                const int i = 4 * part + t;
+                float x = NN_PAD, y = NN_PAD, z = NN_PAD;
+                if (i < tn) { x = rp[3 * i]; y = rp[3 * i + 1]; z = rp[3 * i + 2]; }
+                sx[i] = x; sy[i] = y; sz[i] = z;
+            }
+        } else {
+            for (int i = t; i < fill; i += NN_THREADS) {
+                float x = NN_PAD, y = NN_PAD, z = NN_PAD;
+                if (i < tn) {
+                    const float* p = rp + 3 * (size_t)i;
+                    x = p[0]; y = p[1]; z = p[2];
+                }
+                sx[i] = x; sy[i] = y; sz[i] = z;
+            }
         }
         __syncthreads();
         // this group's sub-range of the tile, in chunks of NN_CHUNK
@@ -308,6 +336,9 @@ int fwd_dispatch(const NNFwdArgs& a, int nseg, int max_a, int max_b, hipStream_t
     const bool all = URED_NN_TILE_ALL && max_r <= NN_TILE_ALL;
     if (!all && (waves1 >= 4096 || max_r < NN_TILE)) launch_fwd<2, 1>(a, max_q, max_r, nseg, ndirs, st);
     else if (!all && waves1 >= 2048) launch_fwd<2, 2>(a, max_q, max_r, nseg, ndirs, st);
+    // whole-set tile over 2048 refs: eight ref groups (512 refs each); 32 x 4096 x 2048 both
+    // directions <2,8> 77 us vs <2,4> 99 (at 2048 refs <2,4> stays ahead: 44 vs 46)
+    else if (all && waves1 >= 512 && max_r > 2048) launch_fwd<2, 8>(a, max_q, max_r, nseg, ndirs, st);
     else if (waves1 >= 512 || !all) launch_fwd<2, 4>(a, max_q, max_r, nseg, ndirs, st);
     else if (waves1 >= 256) launch_fwd<1, 4>(a, max_q, max_r, nseg, ndirs, st);
     else launch_fwd<1, 8>(a, max_q, max_r, nseg, ndirs, st);
