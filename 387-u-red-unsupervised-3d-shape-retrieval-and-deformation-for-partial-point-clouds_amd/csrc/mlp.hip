@@ -1070,7 +1070,12 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
 #pragma unroll
                 for (int j = 0; j < 16; ++j) a[tm][j] = (k0 + 16 * h + j < kend) ? a[tm][j] : 0.f;
         }
-        // ---- MFMAs
+        // ---- MFMAs. s_setprio(1) around the cluster keeps hipcc from moving MFMAs out of it, in
+        // among the next step's loads (cdna_hip_programming.md T5): forward, wgrad and store
+        // variants +1-2 % isolated (tools/ab_libs_step.sh, same box, two rounds); the BN-backward
+        // dgrad went -1..+1 %, so it keeps the plain schedule
+        constexpr bool PRIO = EPI != URED_EPI_BNBWD;
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[0][j], acc[0][0], 0, 0, 0);
@@ -1080,6 +1085,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             if (URED_DMA_SPREAD && next && j == 1) issue_a(stage ^ 1, k0 + BK);
             if (URED_DMA_SPREAD && next && j == 5) issue_b(stage ^ 1, k0 + BK);
         }
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
         stage ^= 1;
     }
 
