@@ -1075,6 +1075,10 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         // variants +1-2 % isolated (tools/ab_libs_step.sh, same box, two rounds); the BN-backward
         // dgrad went -1..+1 %, so it keeps the plain schedule
         constexpr bool PRIO = EPI != URED_EPI_BNBWD;
+        // MFMA group (of 16) behind which the next step's A / B halves are issued: 6 / 11 for the
+        // k-major wgrad (+1.5-2 % isolated, tools/ab_libs_step.sh), 1 / 5 elsewhere (later issue
+        // points measured neutral to negative there)
+        constexpr int DMA_JA = (A_KM && B_KM) ? 6 : 1, DMA_JB = (A_KM && B_KM) ? 11 : 5;
         if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -1082,8 +1086,8 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[1][j], acc[0][1], 0, 0, 0);
             acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[0][j], acc[1][0], 0, 0, 0);
             acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][j], acc[1][1], 0, 0, 0);
-            if (URED_DMA_SPREAD && next && j == 1) issue_a(stage ^ 1, k0 + BK);
-            if (URED_DMA_SPREAD && next && j == 5) issue_b(stage ^ 1, k0 + BK);
+            if (URED_DMA_SPREAD && next && j == DMA_JA) issue_a(stage ^ 1, k0 + BK);
+            if (URED_DMA_SPREAD && next && j == DMA_JB) issue_b(stage ^ 1, k0 + BK);
         }
         if (PRIO) __builtin_amdgcn_s_setprio(0);
         stage ^= 1;
