@@ -1075,10 +1075,10 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         // variants +1-2 % isolated (tools/ab_libs_step.sh, same box, two rounds); the BN-backward
         // dgrad went -1..+1 %, so it keeps the plain schedule
         constexpr bool PRIO = EPI != URED_EPI_BNBWD;
-        // MFMA group (of 16) behind which the next step's A / B halves are issued: 6 / 11 for the
-        // k-major wgrad (+1.5-2 % isolated, tools/ab_libs_step.sh), 1 / 5 elsewhere (later issue
-        // points measured neutral to negative there)
-        constexpr int DMA_JA = (A_KM && B_KM) ? 6 : 1, DMA_JB = (A_KM && B_KM) ? 11 : 5;
+        // MFMA group (of 16) behind which the next step's A / B halves are issued: 6 / 11 with a
+        // k-major B (wgrad +1-2 %, BN-backward dgrad +0.2-1.3 % isolated on the large layers,
+        // profiles/r4zh_*), 1 / 5 with a row-major B (later points neutral to negative there)
+        constexpr int DMA_JA = B_KM ? 6 : 1, DMA_JB = B_KM ? 11 : 5;
         if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
