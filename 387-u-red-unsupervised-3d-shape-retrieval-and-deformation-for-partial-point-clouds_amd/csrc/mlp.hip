@@ -220,6 +220,12 @@ __host__ __device__ __forceinline__ size_t part_idx(int q, int col, int blk, int
     return ((size_t)q * N + col) * nblk + blk;
 }
 
+// Debug build (-DURED_DEBUG_BOUNDS=1): every LDS-DMA destination range and every epilogue
+// buffer-store offset is checked against its allocation on the device (trap on violation).
+#ifndef URED_DEBUG_BOUNDS
+#define URED_DEBUG_BOUNDS 0
+#endif
+
 // ---- shared epilogue ---------------------------------------------------------
 // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
 #define RED(a, q, c) red_f[((a) * 2 + (q)) * BN + (c)]
@@ -243,10 +249,12 @@ template <bool BUF>
 struct OutTile {
     float* base; int ld;
     unsigned ld4;        // row pitch in bytes, laundered per tile (see below)
+    unsigned nrec;       // num_records of the descriptor (bytes)
     __amdgpu_buffer_rsrc_t rsrc;
     __device__ OutTile(float* b, int ld_, int M, int N) : base(b), ld(ld_) {
         if constexpr (BUF) {
-            rsrc = __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)(((long long)(M - 1) * ld_ + N) * 4), 0x00020000);
+            nrec = (unsigned)(((long long)(M - 1) * ld_ + N) * 4);
+            rsrc = __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)nrec, 0x00020000);
             // opaque to the optimiser: keeps the 64 per-element row products from being
             // hoisted out of the persistent tile loop (and spilled)
             ld4 = (unsigned)ld_ * 4u;
@@ -257,6 +265,9 @@ struct OutTile {
         if constexpr (BUF) {
             // 32-bit byte offset (buf_ok guarantees M * ld * 4 < 2^31) and a select: no branch
             const unsigned off = (unsigned)row * ld4 + (unsigned)col * 4u;
+#if URED_DEBUG_BOUNDS
+            if (ok && (row < 0 || col < 0 || off + 4u > nrec)) __builtin_trap();
+#endif
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc, ok ? off : ST_OOB, 0, 0);
         } else if (ok) {
             base[(size_t)row * ld + col] = v;
@@ -360,6 +371,10 @@ __device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2]
                     g = (__builtin_fmaf(y, sc_[j], sh_[j]) > 0.f) ? dh : 0.f;
                     xh = (y - mu_[j]) * is_[j];
                 }
+#if URED_DEBUG_BOUNDS
+                if ((unsigned long long)vo + roff(i, r, lc) + 4u > (unsigned long long)(((long long)(d.M - 1) * d.ldc + d.N) * 4) ||
+                    r0 + (unsigned)(i * 32 + (r & 3) + 8 * (r >> 2)) >= (unsigned)d.M) __builtin_trap();
+#endif
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, g), cr, vo, roff(i, r, lc), 0);
                 a1 += g;
                 a2 += g * xh;
@@ -822,6 +837,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 struct BufOperand {
     i32x4 rsrc;          // raw buffer descriptor: base, stride 0, num_records (bytes), dword3
+    __amdgpu_buffer_rsrc_t rs;   // the same descriptor as the builtins' type
     unsigned vo[4];
 };
 
@@ -839,6 +855,7 @@ template <bool KM>
 __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld, int ext, int e0, int K, int w, int lane) {
     const long long bytes = KM ? ((long long)(K - 1) * ld + ext) * 4 : ((long long)(ext - 1) * ld + K) * 4;
     o.rsrc = make_rsrc(G, bytes);
+    o.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)bytes, BUF_DWORD3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int c = (w * 4 + i) * 64 + lane;
@@ -854,15 +871,21 @@ __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld,
     }
 }
 
-// The DMA is issued from inline asm on purpose: the compiler's waitcnt pass then does not
-// track it, so it adds no vmcnt(0) of its own in front of later ds_reads of the stages (it
-// cannot tell the two stages apart, nor count the epilogue's stores behind the prefetch).
-// Completion is ordered explicitly by the K-loop's vmcnt wait before its barrier. Ops the
-// pass cannot see only make its own vmcnt(N) waits conservative (in-order counter).
-// One asm block issues a wave's four 1-KB chunks of an operand image: m0 (the LDS
-// destination) is set once from a wave-uniform SGPR byte address and advanced by 1 KB with
-// scalar adds — no per-DMA readfirstlane / generic->LDS pointer conversion — and restored.
-// An s_nop follows each m0 write (SALU m0 write -> LDS-DMA hazard).
+// The DMA is issued with the compiler's own LDS-DMA builtin (round 5): hipcc then sets M0
+// itself, pads the SALU-M0-write -> LDS-DMA hazard, and counts every DMA in its vmcnt
+// bookkeeping (cdna_hip_programming.md §5.7: "where a __builtin_amdgcn_* exists, prefer it").
+// Rounds 2-4 issued it from inline asm that saved, advanced and restored M0 itself, invisible
+// to the hazard recognizer and the waitcnt pass; that form was in every tree on which the
+// 8-process config-5 test aborted with HSA_STATUS_ERROR_ILLEGAL_INSTRUCTION ("The
+// multi-process fault"). URED_DMA_ASM=1 rebuilds the old form for A/B only.
+// Cross-wave completion is still ordered explicitly: each wave waits for its own DMA
+// (vmcnt(0)) before the K-loop's barrier; the compiler only sees this wave's reads.
+#ifndef URED_DMA_ASM
+#define URED_DMA_ASM 0
+#endif
+constexpr unsigned GEMM2_SMEM_BYTES = 2u * 2u * (unsigned)(BM * BK) * 4u;   // both stages, A|B images
+
+#if URED_DMA_ASM
 __device__ __forceinline__ void dma4(const i32x4& rsrc, unsigned v0, unsigned v1, unsigned v2, unsigned v3,
                                      unsigned lds) {
     unsigned saved;
@@ -883,12 +906,25 @@ __device__ __forceinline__ void dma4(const i32x4& rsrc, unsigned v0, unsigned v1
         "s_mov_b32 m0, %0"
         : "=&s"(saved) : "s"(lds), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(rsrc) : "memory", "scc");
 }
+#endif
 
-// lds: wave-uniform LDS byte address of this wave's first chunk of the operand image
+// One wave's four 1-KB chunks of an operand image. smem: the stage images' LDS object;
+// off: wave-uniform byte offset of this wave's first chunk inside it.
 template <bool KM>
-__device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, unsigned lds) {
+__device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, float* smem, unsigned off) {
     const unsigned toff = KM ? (unsigned)k0 * (unsigned)ld * 4u : (unsigned)k0 * 4u;
+#if URED_DEBUG_BOUNDS
+    if (off + 4u * 1024u > GEMM2_SMEM_BYTES || (off & 1023u)) __builtin_trap();
+#endif
+#if URED_DMA_ASM
+    const unsigned lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem + off;
     dma4(o.rsrc, o.vo[0] + toff, o.vo[1] + toff, o.vo[2] + toff, o.vo[3] + toff, lds);
+#else
+    char* base = reinterpret_cast<char*>(smem) + off;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(o.rs, (lds_void_t*)(base + i * 1024), 16, o.vo[i] + toff, 0, 0, 0);
+#endif
 }
 
 template <int PRO>
@@ -941,16 +977,15 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     buf_setup<A_KM>(ba, d.A, d.lda, d.M, m0, A_KM ? kend : min(kend, d.k1), w, lane);
     if (!A_KM && has_a2) buf_setup<false>(ba2, d.A2, d.lda2, d.M, m0, d.K - d.k1, w, lane);
     buf_setup<B_KM>(bb, d.B, d.ldb, d.N, n0, kend, w, lane);
-    // this wave's chunk base in the LDS images, as a wave-uniform byte address (SGPR)
-    const unsigned lds_w = __builtin_amdgcn_readfirstlane(
-        (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem + (unsigned)w * 4096u);
+    // this wave's chunk offset in the LDS images, wave-uniform (SGPR)
+    const unsigned lds_w = (unsigned)__builtin_amdgcn_readfirstlane(w) * 4096u;
     auto issue_a = [&](int stage, int k0) {
         const unsigned la = lds_w + (unsigned)stage * (2u * TILE * 4u);
-        if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false>(ba2, d.lda2, k0 - d.k1, la);
-        else buf_tile<A_KM>(ba, d.lda, k0, la);
+        if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false>(ba2, d.lda2, k0 - d.k1, smem, la);
+        else buf_tile<A_KM>(ba, d.lda, k0, smem, la);
     };
     auto issue_b = [&](int stage, int k0) {
-        buf_tile<B_KM>(bb, d.ldb, k0, lds_w + (unsigned)stage * (2u * TILE * 4u) + TILE * 4u);
+        buf_tile<B_KM>(bb, d.ldb, k0, smem, lds_w + (unsigned)stage * (2u * TILE * 4u) + TILE * 4u);
     };
 
     if constexpr (PRO_IN_LDS) {   // visible after the first loop barrier
@@ -995,7 +1030,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         // wave ~60 cycles among MFMAs, 100-185 beside the step's ds_reads; measured on the
         // bare loop: 139 -> 146 TF/s, tools/mfma_clock.hip)
         const bool next = k0 + BK < kend;
-        if (!URED_DMA_SPREAD && next) { issue_a(stage ^ 1, k0 + BK); issue_b(stage ^ 1, k0 + BK); }
+        if (URED_DMA_SPREAD == 0 && next) { issue_a(stage ^ 1, k0 + BK); issue_b(stage ^ 1, k0 + BK); }
 
         // the prologue's scale/shift first: LDS reads complete in issue order, so the
         // prologue (and the MFMAs behind it) can start on the first A fragments
@@ -1047,6 +1082,13 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             }
         }
 
+        // URED_DMA_SPREAD == 2: the next step's DMA right behind this step's fragment reads, in
+        // front of every MFMA (the fence keeps the scheduler from sinking it among them)
+        if (URED_DMA_SPREAD == 2 && next) {
+            issue_a(stage ^ 1, k0 + BK);
+            issue_b(stage ^ 1, k0 + BK);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         // ---- prologues (previous layer's BN+ReLU) and the K tail, on the fragments
         if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
             if (pro_step) {
@@ -1086,8 +1128,8 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[1][j], acc[0][1], 0, 0, 0);
             acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[0][j], acc[1][0], 0, 0, 0);
             acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][j], acc[1][1], 0, 0, 0);
-            if (URED_DMA_SPREAD && next && j == DMA_JA) issue_a(stage ^ 1, k0 + BK);
-            if (URED_DMA_SPREAD && next && j == DMA_JB) issue_b(stage ^ 1, k0 + BK);
+            if (URED_DMA_SPREAD == 1 && next && j == DMA_JA) issue_a(stage ^ 1, k0 + BK);
+            if (URED_DMA_SPREAD == 1 && next && j == DMA_JB) issue_b(stage ^ 1, k0 + BK);
         }
         if (PRIO) __builtin_amdgcn_s_setprio(0);
         stage ^= 1;

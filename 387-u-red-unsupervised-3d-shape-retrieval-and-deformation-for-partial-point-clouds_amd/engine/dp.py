@@ -197,6 +197,13 @@ class FlatGradReducer:
         if opt.flat_param is None and self._arrival:
             opt.layout_order = list(self._arrival)        # first step: backward's order
         active = opt.prepare()
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            # a captured finish() must not sync (the layout check reads its all-reduced hash on
+            # the host) nor rebuild the buckets (their ranges are baked into the graph): the eager
+            # step of the same key, which always runs before its capture, has done both
+            if self._checked != active or (self.overlap and self._fb_key != active):
+                raise RuntimeError("data-parallel: a layout check or bucket rebuild is pending inside a "
+                                   "graph capture (run the step of this key eagerly first)")
         if self._checked != active:
             # first step, or the set of parameters with a gradient changed (e.g. the residual net
             # joining): every rank must reduce the same ranges — checked again (one tiny
@@ -235,9 +242,7 @@ class DataParallelStep(TrainStep):
         super().__init__(cfg, db, device)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.collect = self.world > 1 or (bool(cfg.get("dp_force_collectives", False)) and dist.is_initialized())
-        if self.collect:
-            import loss.contrast_loss as cl
-            cl.FORCE_GATHER = True
+        self.force_gather = self.collect     # this step's contrastive codes go through the group
         if self.world > 1:
             self.broadcast_state()
         params = []

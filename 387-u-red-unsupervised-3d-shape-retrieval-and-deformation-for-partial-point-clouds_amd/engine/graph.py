@@ -111,10 +111,19 @@ class GraphedStep:
     def _inline(self):
         """Capture the collectives inside the graph (RCCL) instead of splitting at them: the
         contrastive all_gather and the bucketed gradient all-reduce issued from backward's hooks,
-        which then overlaps the rest of the backward on RCCL's stream within one graph."""
+        which then overlaps the rest of the backward on RCCL's stream within one graph.
+
+        Only where it has run on hardware: world size 1 (tests/test_nccl_gpu.py, RCCL initialised,
+        every collective captured and replayed). At world size > 1 the ranks capture at different
+        steps (keys follow each rank's batches), so the inline form rests on every rank's eager
+        collective sequence matching another rank's replayed one; until a multi-GPU RCCL run has
+        checked averaged gradients and parameters against eager steps, world > 1 takes the
+        segmented capture (collectives eagerly between graph segments, the gradient all-reduce
+        after the replay) unless cfg["graph_inline_collectives"] asks for the inline form."""
         import torch.distributed as dist
-        return (getattr(self.inner, "collect", False) and dist.is_initialized()
-                and dist.get_backend() == "nccl")
+        if not (getattr(self.inner, "collect", False) and dist.is_initialized() and dist.get_backend() == "nccl"):
+            return False
+        return dist.get_world_size() == 1 or bool(self.inner.cfg.get("graph_inline_collectives", False))
 
     def _flat(self):
         """FlatAdam: the HIP layers write the gradients into its persistent flat buffer."""

@@ -130,6 +130,7 @@ class TrainStep:
         self._zflip = torch.tensor([1.0, 1.0, -1.0], device=dev)
         # the fused HIP loss head (ured_hip/losshead.py); False: the composed torch + NN-launch form
         self.loss_head = dev.type == "cuda" and cfg.get("loss_head", True)
+        self.force_gather = False    # engine/dp.py: gather the contrastive codes even at world size 1
         # optional SyncBN (ured_hip/syncbn.py): global-batch BN statistics over the ranks
         import torch.distributed as dist
         self.sync_bn = bool(cfg.get("sync_bn", False)) and dist.is_initialized() and dist.get_world_size() > 1
@@ -202,7 +203,8 @@ class TrainStep:
             loss = loss + T["cd_loss_full"] * cfg["use_chamfer_loss"] + T["cd_loss_part"] * cfg["use_chamfer_part_loss"]
         if cfg["use_contrast_loss"] > 0.0:
             T["contrast_loss"] = compute_contrast_loss_loss(target_part_f, codes, contrast_labels,
-                                                            cfg.get("differentiable_gather", False))
+                                                            cfg.get("differentiable_gather", False),
+                                                            self.force_gather)
             loss = loss + T["contrast_loss"] * cfg["use_contrast_loss"]
         if cfg["use_symmetry_loss"] > 0.0:
             if not pair:
@@ -255,11 +257,11 @@ class TrainStep:
                                                          off=re_in.off).view(B, N, 3)
         param = regularization_param(params_full, mask_part) if cfg.get("use_param_loss", 0.0) > 0.0 else None
         contrast_ext = None
-        if gathers() and cfg.get("use_contrast_loss", 0.0) > 0.0:
+        if gathers(self.force_gather) and cfg.get("use_contrast_loss", 0.0) > 0.0:
             # the reference gathers the source codes of every rank (contrast_loss.py:35-58)
             contrast_labels = torch.where(src_labels >= 0, torch.ones_like(src_labels), src_labels)
             contrast_ext = compute_contrast_loss_loss(target_part_f, codes, contrast_labels,
-                                                      cfg.get("differentiable_gather", False))
+                                                      cfg.get("differentiable_gather", False), self.force_gather)
         hi = HeadInputs(x, parts, self.np_per_part, src_labels, pts_u, inv, cfg,
                         gate=cfg.get("use_residuals_reg", 0.0) > 0.0 and epoch > cfg["init_p_m_loss"],
                         bounds=batch.get("part_bounds"))
@@ -468,6 +470,9 @@ class PseudoLabelLoader:
 
     def _labels_async(self, sel):
         """get_labels of the targets `sel` on the side stream -> (pinned host tensor, event)."""
+        # the table and the row map were produced on the default stream: order the side stream
+        # behind it (a no-op wait once they are done)
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._side):
             idx = upload(np.asarray(sel, np.int64), self.device)
             lab = self.table.labels(self._rows_dev.index_select(0, idx))

@@ -25,19 +25,16 @@ def get_rank():
     return dist.get_rank() if is_dist_avail_and_initialized() else 0
 
 
-# engine/dp.py DataParallelStep(cfg["dp_force_collectives"]): gather through the process group even
-# at world size 1 (so a one-GPU box exercises the collective path)
-FORCE_GATHER = False
+def gathers(force=False):
+    """Whether the source codes go through a collective: world > 1, or `force` (engine/dp.py
+    DataParallelStep with cfg["dp_force_collectives"] passes it per step, so a one-GPU box
+    exercises the collective path without changing any other step in the process)."""
+    return get_world_size() > 1 or (force and is_dist_avail_and_initialized())
 
 
-def gathers():
-    """Whether the source codes go through a collective (world > 1, or forced)."""
-    return get_world_size() > 1 or (FORCE_GATHER and is_dist_avail_and_initialized())
-
-
-def all_gather_batch(tensors, differentiable=False):
+def all_gather_batch(tensors, differentiable=False, force=False):
     world = get_world_size()
-    if not gathers():
+    if not gathers(force):
         return tensors
     from ured_hip import collective
     out = []
@@ -56,7 +53,7 @@ LOGIT_SCALE = math.log(1 / 0.07)
 _SCALE32 = float(torch.tensor(LOGIT_SCALE, dtype=torch.float32).exp())
 
 
-def compute_contrast_loss_loss(tgt_part_f, src_f, src_labels, differentiable_gather=False):
+def compute_contrast_loss_loss(tgt_part_f, src_f, src_labels, differentiable_gather=False, force_gather=False):
     bs, num_part = src_f.shape[0], src_f.shape[1]
     t = tgt_part_f.reshape(bs * num_part, -1)
     s = src_f.reshape(bs * num_part, -1)
@@ -66,7 +63,7 @@ def compute_contrast_loss_loss(tgt_part_f, src_f, src_labels, differentiable_gat
     s_e = F.normalize(s, dim=-1, p=2)
     # the reference gathers [t_e, s_e] and discards the gathered t_e (contrast_loss.py:35-58):
     # only the source codes are gathered here (same logits, one collective fewer)
-    (s_all,) = all_gather_batch([s_e], differentiable=differentiable_gather)
+    (s_all,) = all_gather_batch([s_e], differentiable=differentiable_gather, force=force_gather)
     scale = _SCALE32                    # exp(logit scale) rounded to fp32 once, as the fp32 tensor exp would
     if t_e.is_cuda:
         # logits t_e s_all^T on the node GEMM (csrc/node.hip): forward and both backward GEMMs

@@ -166,6 +166,8 @@ def bn(x, P, name, training=True):
 
 
 U32 = 2.0 ** -24          # fp32 unit roundoff
+DEV_TOL = 1e-4            # largest accepted deviation of the other implementation's pooled activations
+NN_DEV_TOL = 1e-3         # ... and of its copy of a point set (the deformed shape: 1e-4 absolute in the step tests)
 
 
 def max_pool(h, pool_idx=None, record=None, gpu_h=None):
@@ -192,8 +194,18 @@ def max_pool(h, pool_idx=None, record=None, gpu_h=None):
     chosen = h.gather(2, idx.unsqueeze(-1)).squeeze(-1)
     gap = (mx - chosen).detach()
     hd = h.detach()
-    bound = ((gpu_h(idx).to(hd.dtype) - chosen.detach()).abs() + (gpu_h(am).to(hd.dtype) - mx.detach()).abs()
-             + 4 * U32 * (mx.detach().abs() + chosen.detach().abs()))
+    dev_w = (gpu_h(idx).to(hd.dtype) - chosen.detach()).abs()
+    dev_m = (gpu_h(am).to(hd.dtype) - mx.detach()).abs()
+    # the deviations the bound is built from must themselves be small: a wrong GPU
+    # activation may not widen the tolerance enough to accept a wrong winner
+    ch_scale = hd.abs().amax(dim=2) + 1e-30
+    dev_rel = (torch.maximum(dev_w, dev_m) / ch_scale)
+    if bool((dev_rel > DEV_TOL).any()):
+        g, c = [int(v) for v in (dev_rel > DEV_TOL).nonzero()[0]]
+        raise AssertionError(f"max-pool tie check: the other implementation's activation at group {g} channel {c} "
+                             f"deviates {float(dev_rel[g, c]):.3e} of the channel scale (> {DEV_TOL:.0e}): "
+                             "its values are wrong, not its tie choice")
+    bound = dev_w + dev_m + 4 * U32 * (mx.detach().abs() + chosen.detach().abs())
     over = idx != am
     bad = gap > bound
     if bool(bad.any()):
@@ -361,6 +373,13 @@ def check_nn_choice(P_q, P_c, j_given, j_own, delta_q, delta_c, name):
     d = (P_q - P_c[bi, j_own]).norm(dim=-1)
     dq = delta_q if torch.is_tensor(delta_q) else torch.zeros_like(d)
     dc = delta_c.unsqueeze(1) if torch.is_tensor(delta_c) else torch.zeros_like(d)
+    # the copy's own deviation must be small next to the point sets' extent (the bound
+    # grows with it, so it may not be what makes a wrong index acceptable)
+    ext = torch.maximum(P_q.abs().amax(), P_c.abs().amax()) + 1e-30
+    worst = float(torch.maximum(dq.max(), dc.max()) / ext) if dq.numel() else 0.0
+    if worst > NN_DEV_TOL:
+        raise AssertionError(f"NN tie check ({name}): the other implementation's copy deviates {worst:.3e} of the "
+                             f"point sets' extent (> {NN_DEV_TOL:.0e}): its points are wrong, not its tie choice")
     bound = (d + dq + dc) * (1 + 4 * U32) + dq + dc
     over = j_given != j_own
     if bool((e > bound).any()):

@@ -42,3 +42,20 @@ def test_nn_choice_bound():
     assert R.NN_TIE_STATS["t"]["near_ties"] == 1
     with pytest.raises(AssertionError, match="not a near-tie"):
         R.check_nn_choice(q, c, given, own, torch.tensor([[1e-8]]), 0, "t")
+
+
+def test_max_pool_rejects_wide_deviation():
+    # the other side's value at its winner is far off: the bound built from it would accept the
+    # wrong winner, so the deviation itself is rejected
+    h = torch.tensor([[[1.0, 3.0, 3.01, 0.5]]], dtype=torch.float64)
+    hg = torch.tensor([[[1.0, 3.5, 3.01, 0.5]]], dtype=torch.float32)
+    with pytest.raises(AssertionError, match="its values are wrong"):
+        R.max_pool(h, torch.tensor([[1]]), {}, _gpu(hg))
+
+
+def test_nn_choice_rejects_wide_copy_deviation():
+    q = torch.tensor([[[0.0, 0.0, 0.0]]], dtype=torch.float64)
+    c = torch.tensor([[[1.0, 0.0, 0.0], [1.1, 0.0, 0.0]]], dtype=torch.float64)
+    own, given = torch.tensor([[0]]), torch.tensor([[1]])
+    with pytest.raises(AssertionError, match="its points are wrong"):
+        R.check_nn_choice(q, c, given, own, torch.tensor([[0.2]]), 0, "t")
