@@ -821,7 +821,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 constexpr unsigned BUF_OOB = 0x80000000u;
 constexpr int PRO_LDS = 1024;            // max prologue channels staged in LDS by gemm2
 #ifndef URED_DMA_SPREAD
-#define URED_DMA_SPREAD 1
+#define URED_DMA_SPREAD 2
 #endif
 constexpr int BUF_DWORD3 = 0x00020000;   // raw buffer, gfx9 family (gfx950)
 

@@ -166,7 +166,7 @@ def bn(x, P, name, training=True):
 
 
 U32 = 2.0 ** -24          # fp32 unit roundoff
-DEV_TOL = 1e-4            # largest accepted deviation of the other implementation's pooled activations
+DEV_TOL = 1e-4            # largest accepted deviation of the other implementation's pooled activations, of the layer scale (measured: <= 1.9e-6, profiles/r5b_gpu_tests.log)
 NN_DEV_TOL = 1e-3         # ... and of its copy of a point set (the deformed shape: 1e-4 absolute in the step tests)
 
 
@@ -198,12 +198,14 @@ def max_pool(h, pool_idx=None, record=None, gpu_h=None):
     dev_m = (gpu_h(am).to(hd.dtype) - mx.detach()).abs()
     # the deviations the bound is built from must themselves be small: a wrong GPU
     # activation may not widen the tolerance enough to accept a wrong winner
-    ch_scale = hd.abs().amax(dim=2) + 1e-30
-    dev_rel = (torch.maximum(dev_w, dev_m) / ch_scale)
+    # activation, relative to the layer's scale in that group (fp32 error follows the magnitudes
+    # the channel was computed from, not the channel's own, possibly near-cancelled, maximum)
+    g_scale = hd.abs().amax(dim=(1, 2)).unsqueeze(1) + 1e-30
+    dev_rel = (torch.maximum(dev_w, dev_m) / g_scale)
     if bool((dev_rel > DEV_TOL).any()):
         g, c = [int(v) for v in (dev_rel > DEV_TOL).nonzero()[0]]
         raise AssertionError(f"max-pool tie check: the other implementation's activation at group {g} channel {c} "
-                             f"deviates {float(dev_rel[g, c]):.3e} of the channel scale (> {DEV_TOL:.0e}): "
+                             f"deviates {float(dev_rel[g, c]):.3e} of the layer scale (> {DEV_TOL:.0e}): "
                              "its values are wrong, not its tie choice")
     bound = dev_w + dev_m + 4 * U32 * (mx.detach().abs() + chosen.detach().abs())
     over = idx != am
@@ -219,7 +221,8 @@ def max_pool(h, pool_idx=None, record=None, gpu_h=None):
         record.update(overridden=int(over.sum()), exact_ties=int((g_o == 0).sum()), near_ties=int((g_o > 0).sum()),
                       max_gap=float(g_o.max()) if g_o.numel() else 0.0,
                       max_gap_rel=float((gap / scale)[over].max()) if g_o.numel() else 0.0,
-                      max_gap_over_bound=float((gap / (bound + 1e-300))[over].max()) if g_o.numel() else 0.0)
+                      max_gap_over_bound=float((gap / (bound + 1e-300))[over].max()) if g_o.numel() else 0.0,
+                      max_dev_rel=float(dev_rel.max()))
     return chosen
 
 

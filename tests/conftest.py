@@ -28,3 +28,17 @@ def dev(built):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+# Multi-process rehearsals that put 4-8 ranks on the test box's one GPU run after every
+# single-process parity test (and the 8-rank one last), so that a failure there — the only place
+# where several processes' kernels share the card — cannot stop `pytest -x` before the parity
+# files have run.
+_LAST = {"test_dp_configs_gpu.py": 2}
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        r = _LAST.get(os.path.basename(str(item.fspath)), 0)
+        return (r, "eight_ranks" in item.name)
+    items[:] = sorted(items, key=rank)       # stable: the default order otherwise

@@ -96,7 +96,8 @@ def tie_report(pool_rec, label=""):
         if "overridden" in r:
             parts.append(f"{n}: {r['overridden']} overridden ({r['exact_ties']} exact ties, {r['near_ties']} near-ties), "
                          f"max gap {r['max_gap']:.2e} ({r['max_gap_rel']:.2e} of the channel max, "
-                         f"{r['max_gap_over_bound']:.2f} of the fp32 bound)")
+                         f"{r['max_gap_over_bound']:.2f} of the fp32 bound; HIP activation deviation "
+                         f"{r['max_dev_rel']:.1e} of the layer scale)")
     for k, st in sorted(ured_ref.NN_TIE_STATS.items()):
         parts.append(f"NN {k}: {st['overridden']} overridden ({st['exact_ties']} exact, {st['near_ties']} near), "
                      f"max {st['max_over_bound']:.2f} of the bound")

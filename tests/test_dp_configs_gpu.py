@@ -113,13 +113,30 @@ def _worker(rank, world, port, bs, npts, q):
         dist.destroy_process_group()
 
 
+# Hardware queues per rank process. Each HIP process opens up to GPU_MAX_HW_QUEUES (4 on the box)
+# queues; eight ranks plus the test process on ONE card then ask the scheduler for ~36 queues,
+# beyond what it maps at once, so it time-slices them with mid-kernel context save/restore — a
+# regime that exists only in this one-GPU rehearsal (production runs one rank per GPU). Two per
+# rank keeps the 8-rank rehearsal at the 4-rank one's queue count ("The multi-process
+# fault").
+RANK_HW_QUEUES = "2"
+
+
 def _run(world, bs, npts):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, bs, npts, q)) for r in range(world)]
-    for p in procs:
-        p.start()
+    old = os.environ.get("GPU_MAX_HW_QUEUES")
+    os.environ["GPU_MAX_HW_QUEUES"] = RANK_HW_QUEUES     # inherited by the spawned ranks only
+    try:
+        for p in procs:
+            p.start()
+    finally:
+        if old is None:
+            os.environ.pop("GPU_MAX_HW_QUEUES", None)
+        else:
+            os.environ["GPU_MAX_HW_QUEUES"] = old
     res = [q.get(timeout=360) for _ in procs]
     for p in procs:
         p.join(timeout=60)
