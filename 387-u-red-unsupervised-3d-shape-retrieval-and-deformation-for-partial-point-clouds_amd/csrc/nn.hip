@@ -229,6 +229,7 @@ struct NNBwdArgs {
     const float* a; const float* b; const int4* segs; int n, m;
     const float* gd_a; const float* gd_b; const int* idx_a; const int* idx_b;
     float* ga; float* gb;
+    int accumulate;      // 1: ga/gb += (the reference contract); 0: ga/gb = (no zero fill needed)
 };
 
 // Gradient for the points of one side of a pair (dir 0: a-points, dir 1: b-points).
@@ -302,7 +303,8 @@ __global__ __launch_bounds__(NN_THREADS) void nn_bwd_kernel(NNBwdArgs args) {
     }
     if (valid) {
         float* o = gP + 3 * (size_t)(p_off + j);
-        o[0] += ax; o[1] += ay; o[2] += az;
+        if (args.accumulate) { ax += o[0]; ay += o[1]; az += o[2]; }
+        o[0] = ax; o[1] = ay; o[2] = az;
     }
 }
 
@@ -898,9 +900,22 @@ int ured_nn_bwd(const float* xyz1, const float* xyz2, int b, int n, int m,
     URED_REQUIRE(b >= 0 && n >= 0 && m >= 0, "ured_nn_bwd: negative size");
     if (b == 0) return 0;
     URED_REQUIRE(xyz1 && xyz2 && idx1 && idx2 && gxyz1 && gxyz2, "ured_nn_bwd: null pointer");
-    NNBwdArgs a{xyz1, xyz2, nullptr, n, m, gd1, gd2, idx1, idx2, gxyz1, gxyz2};
+    NNBwdArgs a{xyz1, xyz2, nullptr, n, m, gd1, gd2, idx1, idx2, gxyz1, gxyz2, 1};
     bwd_dispatch(a, b, n, m, (hipStream_t)stream);
     return ured::launch_status("ured_nn_bwd");
+}
+
+int ured_nn_bwd_set(const float* xyz1, const float* xyz2, int b, int n, int m,
+                    const float* gd1, const float* gd2, const int* idx1, const int* idx2,
+                    float* gxyz1, float* gxyz2, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(b >= 0 && n >= 0 && m >= 0, "ured_nn_bwd_set: negative size");
+    if (b == 0) return 0;
+    URED_REQUIRE(xyz1 && xyz2 && idx1 && idx2 && gxyz1 && gxyz2, "ured_nn_bwd_set: null pointer");
+    URED_REQUIRE(n > 0 && m > 0, "ured_nn_bwd_set: empty point set (the caller zero-fills instead)");
+    NNBwdArgs a{xyz1, xyz2, nullptr, n, m, gd1, gd2, idx1, idx2, gxyz1, gxyz2, 0};
+    bwd_dispatch(a, b, n, m, (hipStream_t)stream);
+    return ured::launch_status("ured_nn_bwd_set");
 }
 
 int ured_nn_seg_fwd(const float* a, const float* b, const int* segs, int nseg,
@@ -928,7 +943,7 @@ int ured_nn_seg_bwd(const float* a, const float* b, const int* segs, int nseg,
     URED_REQUIRE(nseg <= 65535, "ured_nn_seg_bwd: nseg %d exceeds 65535", nseg);
     if (nseg == 0) return 0;
     URED_REQUIRE(a && b && segs && idx_a && idx_b && ga, "ured_nn_seg_bwd: null pointer");
-    NNBwdArgs A{a, b, reinterpret_cast<const int4*>(segs), 0, 0, gd_a, gd_b, idx_a, idx_b, ga, gb};
+    NNBwdArgs A{a, b, reinterpret_cast<const int4*>(segs), 0, 0, gd_a, gd_b, idx_a, idx_b, ga, gb, 1};
     bwd_dispatch(A, nseg, max_a_len, max_b_len, (hipStream_t)stream, gb ? 2 : 1);
     return ured::launch_status("ured_nn_seg_bwd");
 }

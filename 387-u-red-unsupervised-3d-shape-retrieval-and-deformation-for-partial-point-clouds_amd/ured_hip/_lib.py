@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libured_hip.so"
 # URED_LIB: an alternative build of the same ABI (A/B kernel experiments, tools/)
 LIB_PATH = os.environ.get("URED_LIB") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -25,6 +25,7 @@ _SZ = ctypes.c_size_t
 _SIGNATURES = {
     "ured_nn_fwd": [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_nn_bwd": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "ured_nn_bwd_set": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "ured_nn_seg_fwd": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "ured_nn_fwd_workspace": [_I, _I, _I, _I, _I, _I],
     "ured_seg_aabb": [_P, _P, _I, _P, _P],

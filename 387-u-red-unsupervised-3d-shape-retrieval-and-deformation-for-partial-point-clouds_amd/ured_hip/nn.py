@@ -63,12 +63,13 @@ class NNDenseFunction(Function):
         b, n, _ = xyz1.shape
         m = xyz2.shape[1]
         dev = xyz1.device
-        dist1 = torch.empty(b, n, device=dev, dtype=torch.float32)
-        dist2 = torch.empty(b, m, device=dev, dtype=torch.float32)
-        idx1 = torch.empty(b, n, device=dev, dtype=torch.int32)
-        idx2 = torch.empty(b, m, device=dev, dtype=torch.int32)
+        # the four outputs are views of ONE allocation (host cost of the reference-API call)
+        buf = torch.empty(2 * b * (n + m), device=dev, dtype=torch.float32)
+        dist1, dist2 = buf[:b * n].view(b, n), buf[b * n:b * (n + m)].view(b, m)
+        idx1 = buf[b * (n + m):b * (2 * n + m)].view(torch.int32).view(b, n)
+        idx2 = buf[b * (2 * n + m):].view(torch.int32).view(b, m)
         if n == 0 or m == 0:
-            dist1.zero_(); dist2.zero_(); idx1.zero_(); idx2.zero_()
+            buf.zero_()
         else:
             ws, nbytes = _workspace(b, n, m, b * n, b * m, 3, dev)
             _lib.call("ured_nn_fwd_ws", _lib.ptr(xyz1), _lib.ptr(xyz2), b, n, m, 3,
@@ -83,14 +84,16 @@ class NNDenseFunction(Function):
         xyz1, xyz2, idx1, idx2 = ctx.saved_tensors
         b, n, _ = xyz1.shape
         m = xyz2.shape[1]
-        g1 = torch.zeros_like(xyz1)
-        g2 = torch.zeros_like(xyz2)
-        if n and m and (gd1 is not None or gd2 is not None):
-            gd1 = gd1.contiguous() if gd1 is not None else None
-            gd2 = gd2.contiguous() if gd2 is not None else None
-            _lib.call("ured_nn_bwd", _lib.ptr(xyz1), _lib.ptr(xyz2), b, n, m,
-                      _lib.ptr(gd1), _lib.ptr(gd2), _lib.ptr(idx1), _lib.ptr(idx2),
-                      _lib.ptr(g1), _lib.ptr(g2), _lib.stream_of(xyz1))
+        if not (n and m and (gd1 is not None or gd2 is not None)):
+            return torch.zeros_like(xyz1), torch.zeros_like(xyz2)
+        # both gradients in one allocation, every element written by the kernel (no zero fill)
+        gbuf = torch.empty(3 * b * (n + m), device=xyz1.device, dtype=xyz1.dtype)
+        g1, g2 = gbuf[:3 * b * n].view(b, n, 3), gbuf[3 * b * n:].view(b, m, 3)
+        gd1 = gd1.contiguous() if gd1 is not None else None
+        gd2 = gd2.contiguous() if gd2 is not None else None
+        _lib.call("ured_nn_bwd_set", _lib.ptr(xyz1), _lib.ptr(xyz2), b, n, m,
+                  _lib.ptr(gd1), _lib.ptr(gd2), _lib.ptr(idx1), _lib.ptr(idx2),
+                  _lib.ptr(g1), _lib.ptr(g2), _lib.stream_of(xyz1))
         return g1, g2
 
 

@@ -40,7 +40,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 7   /* 7: ured_copy_batch; 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
+#define URED_ABI_VERSION 8   /* 8: ured_nn_bwd_set; 7: ured_copy_batch; 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
@@ -63,6 +63,12 @@ int ured_nn_fwd(const float* xyz1, const float* xyz2, int b, int n, int m, int d
 int ured_nn_bwd(const float* xyz1, const float* xyz2, int b, int n, int m,
                 const float* gd1, const float* gd2, const int* idx1, const int* idx2,
                 float* gxyz1, float* gxyz2, void* stream);
+/* The same gradient WRITTEN instead of accumulated (every element of gxyz1 / gxyz2 is set, so
+ * the caller needs no zero fill; n, m > 0). The autograd Function behind chamfer_3DDist uses it;
+ * ured_nn_bwd keeps the reference's accumulate-into-caller-zeroed-buffers contract. */
+int ured_nn_bwd_set(const float* xyz1, const float* xyz2, int b, int n, int m,
+                    const float* gd1, const float* gd2, const int* idx1, const int* idx2,
+                    float* gxyz1, float* gxyz2, void* stream);
 
 /* Ragged NN over segment pairs. segs is a DEVICE int32 array [nseg][4] =
  * {a_off, a_len, b_off, b_len} in points of the two buffers a [*,3] and b [*,3].

@@ -78,6 +78,29 @@ def test_dense_bwd(unn, dev, b, n, m):
     assert torch.equal(a2.grad, a.grad)
 
 
+@pytest.mark.parametrize("b,n,m", [(4, 100, 200), (2, 3000, 17), (1, 2048, 2048)])
+def test_dense_bwd_set_equals_accumulate(unn, dev, b, n, m):
+    """ured_nn_bwd_set (written gradients, the autograd path) == ured_nn_bwd (accumulated into
+    zeroed buffers, the reference contract) bitwise, whatever the output buffers held before;
+    one-direction gradients (gd2 = NULL) too."""
+    from ured_hip import _lib
+    p1 = torch.from_numpy(_rand((b, n, 3), 31)).to(dev)
+    p2 = torch.from_numpy(_rand((b, m, 3), 32)).to(dev)
+    gd1 = torch.from_numpy(_rand((b, n), 33) - 0.5).to(dev)
+    gd2 = torch.from_numpy(_rand((b, m), 34) - 0.5).to(dev)
+    _, _, i1, i2 = unn.nn_dense(p1, p2)
+    i1, i2 = i1.contiguous(), i2.contiguous()
+    for g2in in (gd2, None):
+        ref1, ref2 = torch.zeros_like(p1), torch.zeros_like(p2)
+        _lib.call("ured_nn_bwd", _lib.ptr(p1), _lib.ptr(p2), b, n, m, _lib.ptr(gd1), _lib.ptr(g2in),
+                  _lib.ptr(i1), _lib.ptr(i2), _lib.ptr(ref1), _lib.ptr(ref2), _lib.stream_of(p1))
+        out1 = torch.full_like(p1, float("nan"))
+        out2 = torch.full_like(p2, float("nan"))
+        _lib.call("ured_nn_bwd_set", _lib.ptr(p1), _lib.ptr(p2), b, n, m, _lib.ptr(gd1), _lib.ptr(g2in),
+                  _lib.ptr(i1), _lib.ptr(i2), _lib.ptr(out1), _lib.ptr(out2), _lib.stream_of(p1))
+        assert torch.equal(out1, ref1) and torch.equal(out2, ref2)
+
+
 @pytest.mark.parametrize("n,m", [(3000, 5), (5000, 1), (70, 1300)])
 def test_dense_bwd_degenerate(unn, dev, n, m):
     """Many queries sharing one NN (long per-point contribution lists, > one LDS tile)."""
