@@ -306,12 +306,12 @@ struct InTile {
     }
 };
 
-// BN-backward epilogue of a full 128x128 tile (every row < M, every column < N; no per-element
+// BN-backward epilogue of a full 128 x (64 TN) tile (every row < M, every column < N; no per-element
 // residual gradient, pooled gradients only of 128-row-aligned groups): the general loop below
 // without its per-element bounds selects, and with the Yp loads / G stores addressed as a per-lane
 // buffer offset plus a scalar row offset (no per-element 32-bit multiplies). Same operations in the
 // same order as the general loop, so the results are bitwise the same.
-template <int ACT, bool POOL, class Pre>
+template <int ACT, bool POOL, int TN, class Pre>
 __device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2][2], int m0, int n0, float (&s1)[2],
                                            float (&s2)[2], Pre pre) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
@@ -329,8 +329,8 @@ __device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2]
     };
     float yh[2][2][16];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const unsigned vo = r0 * ly + (unsigned)(n0 + wn * 64 + j * 32 + (lane & 31)) * 4u;
+    for (int j = 0; j < TN; ++j) {
+        const unsigned vo = r0 * ly + (unsigned)(n0 + wn * (32 * TN) + j * 32 + (lane & 31)) * 4u;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -341,16 +341,16 @@ __device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2]
     int pidx_[2];
     const int pg = POOL ? m0 / d.pool_group_rows : 0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+    for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * (32 * TN) + j * 32 + (lane & 31);
         sc_[j] = d.bn_scale[col]; sh_[j] = d.bn_shift[col]; mu_[j] = d.bn_mean[col]; is_[j] = d.bn_invstd[col];
         pidx_[j] = -1; pgr_[j] = 0.f;
         if (POOL) { pidx_[j] = d.pool_idx[(size_t)pg * d.N + col]; pgr_[j] = d.pool_grad[(size_t)pg * d.N + col]; }
     }
     pre();
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const unsigned vo = r0 * lc + (unsigned)(n0 + wn * 64 + j * 32 + (lane & 31)) * 4u;
+    for (int j = 0; j < TN; ++j) {
+        const unsigned vo = r0 * lc + (unsigned)(n0 + wn * (32 * TN) + j * 32 + (lane & 31)) * 4u;
         const int prow = pidx_[j] - (int)r0;       // the pooled winner's row relative to this lane's first row
         float a1 = 0.f, a2 = 0.f;
 #pragma unroll
@@ -385,28 +385,28 @@ __device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2]
     }
 }
 
-template <int EPI, bool BUFST = false, class Pre = NoPre>
+template <int EPI, bool BUFST = false, int TM = 2, int TN = 2, class Pre = NoPre>
 __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2], int m0, int n0,
                                          float* red_f, int* red_i, Pre pre = Pre()) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w & 1, wn = w >> 1;
     // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
-    const int rbase = m0 + wm * 64 + 4 * (lane >> 5);
+    const int rbase = m0 + wm * (32 * TM) + 4 * (lane >> 5);
     auto row_of = [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); };
 
     if (EPI == URED_EPI_STORE || EPI == URED_EPI_SPLITK) {
         OutTile<BUFST> C(d.C + (EPI == URED_EPI_SPLITK ? (size_t)blockIdx.z * d.M * d.ldc : 0), d.ldc, d.M, d.N);
         float bsv[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * (32 * TN) + j * 32 + (lane & 31);
             bsv[j] = (EPI == URED_EPI_STORE && d.bias && col < d.N) ? d.bias[col] : 0.f;
         }
         pre();
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * (32 * TN) + j * 32 + (lane & 31);
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = row_of(i, r);
@@ -427,21 +427,21 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         OutTile<BUFST> Cw(d.C, d.ldc, d.M, d.N);
         float bsv_[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * (32 * TN) + j * 32 + (lane & 31);
             const bool cv = col < d.N;
             bsv_[j] = (cv && d.bias) ? d.bias[col] : 0.f;
             if (rb_blk && cv) bsv_[j] += d.rowbias[(size_t)(m0 / d.group_rows) * d.ldr + col];
         }
         pre();
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * (32 * TN) + j * 32 + (lane & 31);
             const bool cv = col < d.N;
             const float bsv = bsv_[j];
             if (!d.rowbias || rb_blk) {   // common case: no per-element branch or load
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int row = row_of(i, r);
@@ -451,7 +451,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                     }
             } else {
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = row_of(i, r);
@@ -470,10 +470,10 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         // pass 1: column sums of p over valid rows
         float csum[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < TN; ++j) {
             float s = 0.f;
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float p = fmaxf(acc[i][j][r], plo);
@@ -484,22 +484,22 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         }
         if (lane < 32) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) RED(wm, 0, wn * 64 + j * 32 + lane) = csum[j];
+            for (int j = 0; j < TN; ++j) RED(wm, 0, wn * (32 * TN) + j * 32 + lane) = csum[j];
         }
         lds_barrier();
         float cmean[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int c = wn * 64 + j * 32 + (lane & 31);
+        for (int j = 0; j < TN; ++j) {
+            const int c = wn * (32 * TN) + j * 32 + (lane & 31);
             cmean[j] = (RED(0, 0, c) + RED(1, 0, c)) / (float)nvalid;
         }
         // pass 2: M2 about the block mean
         float cm2[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < TN; ++j) {
             float s = 0.f;
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const float p = fmaxf(acc[i][j][r], plo);
@@ -511,13 +511,13 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         }
         if (lane < 32) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) RED(wm, 1, wn * 64 + j * 32 + lane) = cm2[j];
+            for (int j = 0; j < TN; ++j) RED(wm, 1, wn * (32 * TN) + j * 32 + lane) = cm2[j];
         }
         lds_barrier();
         if (wm == 0 && lane < 32) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int c = wn * 64 + j * 32 + lane;
+            for (int j = 0; j < TN; ++j) {
+                const int c = wn * (32 * TN) + j * 32 + lane;
                 const int col = n0 + c;
                 if (col < d.N) {
                     d.stat_ws[part_idx(0, col, blk, d.N, d.M)] = cmean[j];
@@ -531,10 +531,10 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             float mx[2], mn[2];
             int ix[2], in_[2];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int j = 0; j < TN; ++j) {
                 mx[j] = -__builtin_inff(); mn[j] = __builtin_inff(); ix[j] = 0x7fffffff; in_[j] = 0x7fffffff;
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int row = row_of(i, r);
@@ -550,8 +550,8 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             }
             if (lane < 32) {
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int c = wn * 64 + j * 32 + lane;
+                for (int j = 0; j < TN; ++j) {
+                    const int c = wn * (32 * TN) + j * 32 + lane;
                     RED(wm, 0, c) = mx[j]; REDI(wm, 0, c) = ix[j];
                     RED(wm, 1, c) = mn[j]; REDI(wm, 1, c) = in_[j];
                 }
@@ -559,8 +559,8 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             lds_barrier();
             if (wm == 0 && lane < 32) {
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int c = wn * 64 + j * 32 + lane;
+                for (int j = 0; j < TN; ++j) {
+                    const int c = wn * (32 * TN) + j * 32 + lane;
                     const int col = n0 + c;
                     if (col >= d.N) continue;
                     float a = RED(0, 0, c); int ai = REDI(0, 0, c);
@@ -579,16 +579,16 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
     if (EPI == URED_EPI_BNBWD) {
         float s1[2], s2[2];
         const bool pool_al = d.pool_idx && (d.pool_group_rows % BM == 0);
-        const bool full = BUFST && m0 + BM <= d.M && n0 + BN <= d.N && !d.gadd && (!d.pool_idx || pool_al);
+        const bool full = BUFST && m0 + 64 * TM <= d.M && n0 + 64 * TN <= d.N && !d.gadd && (!d.pool_idx || pool_al);
         if (full) {
             if (pool_al) {
-                if (d.bwd_res == URED_ACT_RES) bnbwd_full<URED_ACT_RES, true>(d, acc, m0, n0, s1, s2, pre);
-                else if (d.bwd_res == URED_ACT_BN) bnbwd_full<URED_ACT_BN, true>(d, acc, m0, n0, s1, s2, pre);
-                else bnbwd_full<URED_ACT_ENC, true>(d, acc, m0, n0, s1, s2, pre);
+                if (d.bwd_res == URED_ACT_RES) bnbwd_full<URED_ACT_RES, true, TN>(d, acc, m0, n0, s1, s2, pre);
+                else if (d.bwd_res == URED_ACT_BN) bnbwd_full<URED_ACT_BN, true, TN>(d, acc, m0, n0, s1, s2, pre);
+                else bnbwd_full<URED_ACT_ENC, true, TN>(d, acc, m0, n0, s1, s2, pre);
             } else {
-                if (d.bwd_res == URED_ACT_RES) bnbwd_full<URED_ACT_RES, false>(d, acc, m0, n0, s1, s2, pre);
-                else if (d.bwd_res == URED_ACT_BN) bnbwd_full<URED_ACT_BN, false>(d, acc, m0, n0, s1, s2, pre);
-                else bnbwd_full<URED_ACT_ENC, false>(d, acc, m0, n0, s1, s2, pre);
+                if (d.bwd_res == URED_ACT_RES) bnbwd_full<URED_ACT_RES, false, TN>(d, acc, m0, n0, s1, s2, pre);
+                else if (d.bwd_res == URED_ACT_BN) bnbwd_full<URED_ACT_BN, false, TN>(d, acc, m0, n0, s1, s2, pre);
+                else bnbwd_full<URED_ACT_ENC, false, TN>(d, acc, m0, n0, s1, s2, pre);
             }
         } else {
         // Yp one column half (32 values) at a time: the j = 0 half and the per-column
@@ -601,9 +601,9 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         f16v yh[URED_BNBWD_YALL ? 2 : 1][2];
         InTile<BUFST> Yr(d.Yp, d.ldy, d.M, d.N);
         auto load_y = [&](int j) {
-            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+            const int col = n0 + wn * (32 * TN) + j * 32 + (lane & 31);
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) yh[URED_BNBWD_YALL ? j : 0][i][r] = Yr.get(row_of(i, r), col);
         };
@@ -614,8 +614,8 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         float sc_[2], sh_[2], mu_[2], is_[2], pgr_[2];
         int pidx_[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * (32 * TN) + j * 32 + (lane & 31);
             const bool cv = col < d.N;
             const int cc = cv ? col : 0;
             sc_[j] = d.bn_scale[cc]; sh_[j] = d.bn_shift[cc]; mu_[j] = d.bn_mean[cc]; is_[j] = d.bn_invstd[cc];
@@ -631,9 +631,9 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         const bool relu_mask = d.bwd_res != URED_ACT_RES && d.bwd_res != URED_ACT_BN;
         const float ylo = d.bwd_res == URED_ACT_RES ? 0.f : -__builtin_inff();
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < TN; ++j) {
             if (!URED_BNBWD_YALL && j == 1) load_y(1);
-            const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+            const int col = n0 + wn * (32 * TN) + j * 32 + (lane & 31);
             const bool cv = col < d.N;
             const float sc = sc_[j], sh = sh_[j], mu = mu_[j], is = is_[j];
             const int pidx = pidx_[j];
@@ -645,7 +645,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                 // the block's pooled gradient as a select (pidx = -1 matches no row)
                 const float sck = relu_mask ? sc : 0.f, shk = relu_mask ? sh : 1.f;
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         const int row = row_of(i, r);
@@ -661,7 +661,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                     }
             } else {
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = row_of(i, r);
@@ -698,16 +698,16 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
         }   // general loop
         if (lane < 32) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                RED(wm, 0, wn * 64 + j * 32 + lane) = s1[j];
-                RED(wm, 1, wn * 64 + j * 32 + lane) = s2[j];
+            for (int j = 0; j < TN; ++j) {
+                RED(wm, 0, wn * (32 * TN) + j * 32 + lane) = s1[j];
+                RED(wm, 1, wn * (32 * TN) + j * 32 + lane) = s2[j];
             }
         }
         lds_barrier();
         if (wm == 0 && lane < 32) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int c = wn * 64 + j * 32 + lane;
+            for (int j = 0; j < TN; ++j) {
+                const int c = wn * (32 * TN) + j * 32 + lane;
                 const int col = n0 + c;
                 if (col < d.N) {
                     d.bwd_ws[part_idx(0, col, blk, d.N, d.M)] = RED(0, 0, c) + RED(1, 0, c);
@@ -820,6 +820,13 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // k >= K row of a k-major operand: the hardware returns zeros for them.
 constexpr unsigned BUF_OOB = 0x80000000u;
 constexpr int PRO_LDS = 1024;            // max prologue channels staged in LDS by gemm2
+// 64-wide block tiles for the narrow layers (gemm2_kernel TM / TN); 0 = 128 x 128 everywhere
+#ifndef URED_GEMM_NARROW
+#define URED_GEMM_NARROW 1
+#endif
+// Where a K-step issues the next step's LDS-DMA: 0 = before its fragment reads, 1 = in two
+// halves between MFMA groups (rounds 3-4), 2 = right behind its fragment reads, ahead of every
+// MFMA (round 5 default: DESIGN.md, "The multi-process fault"; 0.9 % of the step vs 1)
 #ifndef URED_DMA_SPREAD
 #define URED_DMA_SPREAD 2
 #endif
@@ -833,38 +840,29 @@ __host__ __device__ inline bool buf_ok(const UredGemmDesc& d) {
         (d.b_kmajor ? (long long)d.K * d.ldb : (long long)d.N * d.ldb) * 4 < 0x7fffffffLL;
 }
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-
 struct BufOperand {
-    i32x4 rsrc;          // raw buffer descriptor: base, stride 0, num_records (bytes), dword3
-    __amdgpu_buffer_rsrc_t rs;   // the same descriptor as the builtins' type
-    unsigned vo[4];
+    __amdgpu_buffer_rsrc_t rs;   // raw buffer descriptor: base, stride 0, num_records (bytes)
+    unsigned vo[4];              // per-lane byte offsets of the wave's pieces
 };
 
-__device__ __forceinline__ i32x4 make_rsrc(const void* base, long long bytes) {
-    const unsigned long long b = reinterpret_cast<unsigned long long>(base);
-    i32x4 r;
-    r.x = (int)(unsigned)(b & 0xffffffffull);
-    r.y = (int)(unsigned)((b >> 32) & 0xffffull);
-    r.z = (int)(unsigned)bytes;
-    r.w = BUF_DWORD3;
-    return r;
-}
-
-template <bool KM>
+// NP = EXT / 32: 16-B chunks per wave-lane of an EXT-wide operand image (EXT = 128 or 64 rows /
+// columns), i.e. the number of 1-KB DMA pieces each of the 4 waves issues per image. Wave w
+// issues chunks [w*NP*64, (w+1)*NP*64): row-major image chunk c = (row c>>3, slot c&7), k-major
+// image chunk c = (k = c / (EXT/4), 4 columns at 4*(c % (EXT/4))).
+template <bool KM, int EXT>
 __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld, int ext, int e0, int K, int w, int lane) {
+    constexpr int NP = EXT / 32, CPR = EXT / 4;
     const long long bytes = KM ? ((long long)(K - 1) * ld + ext) * 4 : ((long long)(ext - 1) * ld + K) * 4;
-    o.rsrc = make_rsrc(G, bytes);
     o.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)bytes, BUF_DWORD3);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int c = (w * 4 + i) * 64 + lane;
+    for (int i = 0; i < NP; ++i) {
+        const int c = (w * NP + i) * 64 + lane;
         if constexpr (!KM) {
             const int r = c >> 3, p = c & 7, sl = p ^ ((r >> 1) & 7);
             const int row = e0 + r;
             o.vo[i] = row < ext ? (unsigned)(((long long)row * ld + 4 * sl) * 4) : BUF_OOB;
         } else {
-            const int kk = c >> 5, c4 = c & 31;
+            const int kk = c / CPR, c4 = c % CPR;
             const int col = e0 + 4 * c4;
             o.vo[i] = col < ext ? (unsigned)(((long long)kk * ld + col) * 4) : BUF_OOB;
         }
@@ -877,54 +875,23 @@ __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld,
 // Rounds 2-4 issued it from inline asm that saved, advanced and restored M0 itself, invisible
 // to the hazard recognizer and the waitcnt pass; that form was in every tree on which the
 // 8-process config-5 test aborted with HSA_STATUS_ERROR_ILLEGAL_INSTRUCTION ("The
-// multi-process fault"). URED_DMA_ASM=1 rebuilds the old form for A/B only.
+// multi-process fault"; its A/B numbers: profiles/r5a_dma_form_gemm_ab.log).
 // Cross-wave completion is still ordered explicitly: each wave waits for its own DMA
-// (vmcnt(0)) before the K-loop's barrier; the compiler only sees this wave's reads.
-#ifndef URED_DMA_ASM
-#define URED_DMA_ASM 0
-#endif
+// (vmcnt) before the K-loop's barrier; the compiler only sees this wave's reads.
 constexpr unsigned GEMM2_SMEM_BYTES = 2u * 2u * (unsigned)(BM * BK) * 4u;   // both stages, A|B images
 
-#if URED_DMA_ASM
-__device__ __forceinline__ void dma4(const i32x4& rsrc, unsigned v0, unsigned v1, unsigned v2, unsigned v3,
-                                     unsigned lds) {
-    unsigned saved;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %1\n\t"
-        "s_nop 0\n\t"
-        "buffer_load_dwordx4 %2, %6, 0 offen lds\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "buffer_load_dwordx4 %3, %6, 0 offen lds\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "buffer_load_dwordx4 %4, %6, 0 offen lds\n\t"
-        "s_add_u32 m0, m0, 0x400\n\t"
-        "s_nop 0\n\t"
-        "buffer_load_dwordx4 %5, %6, 0 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(saved) : "s"(lds), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(rsrc) : "memory", "scc");
-}
-#endif
-
-// One wave's four 1-KB chunks of an operand image. smem: the stage images' LDS object;
-// off: wave-uniform byte offset of this wave's first chunk inside it.
-template <bool KM>
+// One wave's NP 1-KB pieces of an operand image. smem: the stage images' LDS object; off:
+// wave-uniform byte offset of this wave's first piece inside it.
+template <bool KM, int NP>
 __device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, float* smem, unsigned off) {
     const unsigned toff = KM ? (unsigned)k0 * (unsigned)ld * 4u : (unsigned)k0 * 4u;
 #if URED_DEBUG_BOUNDS
-    if (off + 4u * 1024u > GEMM2_SMEM_BYTES || (off & 1023u)) __builtin_trap();
+    if (off + NP * 1024u > GEMM2_SMEM_BYTES || (off & 1023u)) __builtin_trap();
 #endif
-#if URED_DMA_ASM
-    const unsigned lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem + off;
-    dma4(o.rsrc, o.vo[0] + toff, o.vo[1] + toff, o.vo[2] + toff, o.vo[3] + toff, lds);
-#else
     char* base = reinterpret_cast<char*>(smem) + off;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NP; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(o.rs, (lds_void_t*)(base + i * 1024), 16, o.vo[i] + toff, 0, 0, 0);
-#endif
 }
 
 template <int PRO>
@@ -934,9 +901,17 @@ __device__ __forceinline__ float pro_v(float x, float s, float t) {
     return x;
 }
 
-template <bool A_KM, bool B_KM, int PRO_A, int PRO_B, int EPI>
+// TM / TN: 32-row / 32-column MFMA tiles per wave (2 x 2 waves per block), so the block tile is
+// (64 TM) x (64 TN): 128 x 128 for the wide layers; TN = 1 (128 x 64) for outputs of <= 64
+// columns and TM = 1 (64 x ...) for split-K / store GEMMs of <= 64 output rows — the 32- and
+// 64-channel layers, where a 128-wide tile spent half to three quarters of its MFMAs on zeros.
+template <bool A_KM, bool B_KM, int PRO_A, int PRO_B, int EPI, int TM, int TN>
 __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
-    constexpr int TILE = BM * BK;                  // floats per operand image
+    static_assert(TM == 2 || EPI == URED_EPI_SPLITK || EPI == URED_EPI_STORE,
+                  "64-row tiles only for epilogues without 128-row block partials");
+    constexpr int TILE = BM * BK;                  // floats per (largest) operand image
+    constexpr int BMT = 64 * TM, BNT = 64 * TN;    // this instance's block tile
+    constexpr int NPA = BMT / 32, NPB = BNT / 32;  // 1-KB DMA pieces per wave and image
     // row-major A with a prologue: the per-channel scale/shift vectors (k < k1 <= PRO_LDS)
     // are staged in LDS once, so a tile reads them with broadcast ds_reads instead of
     // waiting on global (L2) latency every K-step
@@ -948,7 +923,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     __shared__ int red_i[4 * BN];
     __shared__ __attribute__((aligned(16))) float pro_lds[PRO_IN_LDS ? 2 * PRO_LDS : 4];   // scale | shift
 
-    const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
+    const int ntm = (d.M + BMT - 1) / BMT, ntn = (d.N + BNT - 1) / BNT;
     const int ntiles = ntm * ntn;
     int kbeg = 0, kend = d.K;
     if (EPI == URED_EPI_SPLITK) {
@@ -964,8 +939,8 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     int m0, n0;
     {
         const int tl = xcd_remap(blockIdx.x, ntiles);
-        m0 = (tl / ntn) * BM;
-        n0 = (tl % ntn) * BN;
+        m0 = (tl / ntn) * BMT;
+        n0 = (tl % ntn) * BNT;
     }
 
     // Operands reach LDS by buffer-descriptor DMA (launch() guarantees buf_ok): a
@@ -974,25 +949,30 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     const bool has_a2 = !A_KM && d.k1 < d.K;
     BufOperand ba, ba2, bb;
     // a k-major operand's rows past kend must read as zero too (split-K: kend < K)
-    buf_setup<A_KM>(ba, d.A, d.lda, d.M, m0, A_KM ? kend : min(kend, d.k1), w, lane);
-    if (!A_KM && has_a2) buf_setup<false>(ba2, d.A2, d.lda2, d.M, m0, d.K - d.k1, w, lane);
-    buf_setup<B_KM>(bb, d.B, d.ldb, d.N, n0, kend, w, lane);
-    // this wave's chunk offset in the LDS images, wave-uniform (SGPR)
-    const unsigned lds_w = (unsigned)__builtin_amdgcn_readfirstlane(w) * 4096u;
+    buf_setup<A_KM, BMT>(ba, d.A, d.lda, d.M, m0, A_KM ? kend : min(kend, d.k1), w, lane);
+    if (!A_KM && has_a2) buf_setup<false, BMT>(ba2, d.A2, d.lda2, d.M, m0, d.K - d.k1, w, lane);
+    buf_setup<B_KM, BNT>(bb, d.B, d.ldb, d.N, n0, kend, w, lane);
+    // this wave's first piece in the A / B images, wave-uniform (SGPR)
+    const unsigned wu = (unsigned)__builtin_amdgcn_readfirstlane(w);
+    const unsigned lds_a = wu * (NPA * 1024u), lds_b = TILE * 4u + wu * (NPB * 1024u);
     auto issue_a = [&](int stage, int k0) {
-        const unsigned la = lds_w + (unsigned)stage * (2u * TILE * 4u);
-        if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false>(ba2, d.lda2, k0 - d.k1, smem, la);
-        else buf_tile<A_KM>(ba, d.lda, k0, smem, la);
+        const unsigned la = lds_a + (unsigned)stage * (2u * TILE * 4u);
+        if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false, NPA>(ba2, d.lda2, k0 - d.k1, smem, la);
+        else buf_tile<A_KM, NPA>(ba, d.lda, k0, smem, la);
     };
     auto issue_b = [&](int stage, int k0) {
-        buf_tile<B_KM>(bb, d.ldb, k0, smem, lds_w + (unsigned)stage * (2u * TILE * 4u) + TILE * 4u);
+        buf_tile<B_KM, NPB>(bb, d.ldb, k0, smem, lds_b + (unsigned)stage * (2u * TILE * 4u));
     };
 
     if constexpr (PRO_IN_LDS) {   // visible after the first loop barrier
         for (int i = t; i < d.k1; i += NT) { pro_lds[i] = d.pro_s[i]; pro_lds[PRO_LDS + i] = d.pro_t[i]; }
     }
     int stage = 0;
+    // a reduction of exactly two K-steps (the 64-channel layers' K = 64) gets both stages'
+    // DMA up front: one memory round trip in front of the MFMAs instead of two
+    const bool both = kend - kbeg > BK && kend - kbeg <= 2 * BK;
     if (kbeg < kend) { issue_a(0, kbeg); issue_b(0, kbeg); }
+    if (both) { issue_a(1, kbeg + BK); issue_b(1, kbeg + BK); }
 
     f16v acc[2][2];
 #pragma unroll
@@ -1006,30 +986,28 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     float bs_[2] = {1.f, 1.f}, bt_[2] = {0.f, 0.f};
     if (PRO_B != URED_PRO_NONE) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            int c = n0 + wn * 64 + j * 32 + li;
+        for (int j = 0; j < TN; ++j) {
+            int c = n0 + wn * (32 * TN) + j * 32 + li;
             c = c < d.N ? c : d.N - 1;
             bs_[j] = d.pro_s[c]; bt_[j] = d.pro_t[c];
         }
         // Re-define the loaded values through an asm so the compiler's wait for these loads
-        // sits here, once, and not inside the K-loop, where the hardware counter also holds
-        // the (compiler-invisible) next-step DMA and a vmcnt(0) would expose it every step.
+        // sits here, once, and not inside the K-loop.
         asm volatile("s_waitcnt vmcnt(0)" : "+v"(bs_[0]), "+v"(bs_[1]), "+v"(bt_[0]), "+v"(bt_[1]));
     }
 
     for (int k0 = kbeg; k0 < kend; k0 += BK) {
-        // this wave's share of the step's DMA must have landed before the barrier
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // this wave's share of the step's DMA must have landed before the barrier (with both
+        // stages in flight, the first step waits only for stage 0's pieces: vmcnt counts in order)
+        if (both && k0 == kbeg) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NPA + NPB) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
         const float* As = smem + stage * 2 * TILE;
         const float* Bs = As + TILE;
         const bool tail = k0 + BK > kend;
         // next step's DMA goes into the other stage (its last readers passed the barrier
-        // above). URED_DMA_SPREAD: its two 4-piece halves are issued between MFMA groups
-        // instead of in one burst in front of the fragment reads (an LDS-DMA piece costs its
-        // wave ~60 cycles among MFMAs, 100-185 beside the step's ds_reads; measured on the
-        // bare loop: 139 -> 146 TF/s, tools/mfma_clock.hip)
-        const bool next = k0 + BK < kend;
+        // above); URED_DMA_SPREAD picks the issue point (see its definition)
+        const bool next = k0 + BK < kend && !both;
         if (URED_DMA_SPREAD == 0 && next) { issue_a(stage ^ 1, k0 + BK); issue_b(stage ^ 1, k0 + BK); }
 
         // the prologue's scale/shift first: LDS reads complete in issue order, so the
@@ -1053,8 +1031,8 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         float a[2][16], b[2][16];
         if constexpr (!A_KM) {
 #pragma unroll
-            for (int tm = 0; tm < 2; ++tm) {
-                const int r = wm * 64 + tm * 32 + li;
+            for (int tm = 0; tm < TM; ++tm) {
+                const int r = wm * (32 * TM) + tm * 32 + li;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const float4 v4 = *reinterpret_cast<const float4*>(As + r * 32 + 4 * ((4 * h + q) ^ ((r >> 1) & 7)));
@@ -1063,13 +1041,13 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             }
         } else {
 #pragma unroll
-            for (int tm = 0; tm < 2; ++tm)
+            for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int j = 0; j < 16; ++j) a[tm][j] = As[(16 * h + j) * BM + wm * 64 + tm * 32 + li];
+                for (int j = 0; j < 16; ++j) a[tm][j] = As[(16 * h + j) * BMT + wm * (32 * TM) + tm * 32 + li];
         }
 #pragma unroll
-        for (int tn = 0; tn < 2; ++tn) {
-            const int cidx = wn * 64 + tn * 32 + li;
+        for (int tn = 0; tn < TN; ++tn) {
+            const int cidx = wn * (32 * TN) + tn * 32 + li;
             if constexpr (!B_KM) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -1078,7 +1056,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                 }
             } else {
 #pragma unroll
-                for (int j = 0; j < 16; ++j) b[tn][j] = Bs[(16 * h + j) * BN + cidx];
+                for (int j = 0; j < 16; ++j) b[tn][j] = Bs[(16 * h + j) * BNT + cidx];
             }
         }
 
@@ -1095,20 +1073,20 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                 // scalar v_fma_f32 + v_max_f32: beside MFMAs a packed v_pk_fma_f32 costs more
                 // issue time than two plain fmas (MI355X_MICROARCH.md, filler prices)
 #pragma unroll
-                for (int tm = 0; tm < 2; ++tm)
+                for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                     for (int j = 0; j < 16; ++j) a[tm][j] = pro_v<PRO_A>(a[tm][j], ss[j], tt[j]);
             }
         }
         if constexpr (B_KM && PRO_B != URED_PRO_NONE) {
 #pragma unroll
-            for (int tn = 0; tn < 2; ++tn)
+            for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
                 for (int j = 0; j < 16; ++j) b[tn][j] = pro_v<PRO_B>(b[tn][j], bs_[tn], bt_[tn]);
         }
         if (tail) {   // zero the k >= K part of the reduction (the images hold clamped copies)
 #pragma unroll
-            for (int tm = 0; tm < 2; ++tm)
+            for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int j = 0; j < 16; ++j) a[tm][j] = (k0 + 16 * h + j < kend) ? a[tm][j] : 0.f;
         }
@@ -1117,17 +1095,17 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         // variants +1-2 % isolated (tools/ab_libs_step.sh, same box, two rounds); the BN-backward
         // dgrad went -1..+1 %, so it keeps the plain schedule
         constexpr bool PRIO = EPI != URED_EPI_BNBWD;
-        // MFMA group (of 16) behind which the next step's A / B halves are issued: 6 / 11 with a
-        // k-major B (wgrad +1-2 %, BN-backward dgrad +0.2-1.3 % isolated on the large layers,
-        // profiles/r4zh_*), 1 / 5 with a row-major B (later points neutral to negative there)
+        // URED_DMA_SPREAD == 1: MFMA group (of 16) behind which the next step's A / B halves are
+        // issued: 6 / 11 with a k-major B, 1 / 5 with a row-major B (profiles/r4zh_*)
         constexpr int DMA_JA = B_KM ? 6 : 1, DMA_JB = B_KM ? 11 : 5;
         if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[0][j], acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][j], b[1][j], acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[0][j], acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][j], b[1][j], acc[1][1], 0, 0, 0);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[tm][j], b[tn][j], acc[tm][tn], 0, 0, 0);
             if (URED_DMA_SPREAD == 1 && next && j == DMA_JA) issue_a(stage ^ 1, k0 + BK);
             if (URED_DMA_SPREAD == 1 && next && j == DMA_JB) issue_b(stage ^ 1, k0 + BK);
         }
@@ -1135,7 +1113,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         stage ^= 1;
     }
 
-    epilogue<EPI, true>(d, acc, m0, n0, red_f, red_i);
+    epilogue<EPI, true, TM, TN>(d, acc, m0, n0, red_f, red_i);
 }
 
 // ---- small kernels -------------------------------------------------------------
@@ -1757,8 +1735,17 @@ void launch(const UredGemmDesc& d, hipStream_t st) {
     if (EPI == URED_EPI_FWD && fwd_small_ok(d)) { launch_fwd_small(d, st); return; }
     const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
     dim3 grid(ntm * ntn, 1, EPI == URED_EPI_SPLITK ? d.splits : 1);
-    if (vec_ok(d) && v2_ok(d) && buf_ok(d))
-        hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI>), grid, dim3(NT), 0, st, d);
+    if (vec_ok(d) && v2_ok(d) && buf_ok(d)) {
+        // narrow tiles for outputs of <= 64 columns (and, split-K / store only, <= 64 rows)
+        constexpr bool NARROW_M = EPI == URED_EPI_SPLITK || EPI == URED_EPI_STORE;
+        const bool tn1 = URED_GEMM_NARROW && d.N <= 64;
+        const bool tm1 = URED_GEMM_NARROW && NARROW_M && d.M <= 64;
+        grid.x = ((d.M + (tm1 ? 63 : 127)) / (tm1 ? 64 : 128)) * ((d.N + (tn1 ? 63 : 127)) / (tn1 ? 64 : 128));
+        if (tm1 && tn1) hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI, NARROW_M ? 1 : 2, 1>), grid, dim3(NT), 0, st, d);
+        else if (tm1) hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI, NARROW_M ? 1 : 2, 2>), grid, dim3(NT), 0, st, d);
+        else if (tn1) hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI, 2, 1>), grid, dim3(NT), 0, st, d);
+        else hipLaunchKernelGGL((gemm2_kernel<A_KM, B_KM, PA, PB, EPI, 2, 2>), grid, dim3(NT), 0, st, d);
+    }
     else if (vec_ok(d)) hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, true>), grid, dim3(NT), 0, st, d);
     else hipLaunchKernelGGL((gemm_kernel<A_KM, B_KM, PA, PB, EPI, false>), grid, dim3(NT), 0, st, d);
 }

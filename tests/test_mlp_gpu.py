@@ -100,6 +100,54 @@ def test_gemm_k3_padded_views(K, dev):
     close(dX, A[:, 2:5] @ Wk[1:4, 2:2 + N], 1e-5, "k3 dgrad")
 
 
+@pytest.mark.parametrize("M,N,Kd", [(1000, 32, 256), (1000, 64, 64), (999, 40, 48), (4096, 64, 96), (130, 3, 64)])
+def test_gemm_narrow_forward(K, dev, M, N, Kd):
+    """Outputs of <= 64 columns take the 128 x 64 block tile (gemm2_kernel TN = 1); K = 33..64 also
+    takes the two-stage-up-front prologue. Store form and the BN-statistics form with both
+    prologues, vs float64."""
+    g = torch.Generator().manual_seed(M + 7 * N + Kd)
+    A = torch.randn(M, Kd, generator=g)
+    W = torch.randn(N, Kd, generator=g)
+    b = torch.randn(N, generator=g)
+    C = torch.empty(M, N, device=dev)
+    K.gemm(M, N, Kd, A.to(dev), Kd, W.to(dev), Kd, C, N, bias=b.to(dev))
+    close(C, A.double() @ W.double().t() + b.double(), 1e-5, "narrow store")
+    for pro in (1, 2):
+        s, t = torch.rand(Kd, generator=g) + 0.5, torch.randn(Kd, generator=g)
+        Y = torch.empty(M, N, device=dev)
+        ws = torch.empty(K.nblocks(M), 2, N, device=dev)
+        K.gemm(M, N, Kd, A.to(dev), Kd, W.to(dev), Kd, Y, N, pro_a=pro, pro_s=s.to(dev), pro_t=t.to(dev),
+               epi=K.EPI_FWD, stat_ws=ws, stat_relu=(pro == 2))
+        h = torch.relu(A.double() * s + t) if pro == 1 else torch.relu(A.double()) * s + t
+        ref = h @ W.double().t()
+        close(Y, ref, 1e-5, f"narrow fwd pro{pro}")
+        st = K.bn_fwd_finalize(ws, M, N, torch.ones(N, device=dev), torch.zeros(N, device=dev), 1e-5, 0.1,
+                               torch.zeros(N, device=dev), torch.ones(N, device=dev))
+        p = torch.relu(ref) if pro == 2 else ref
+        close(st.mean, p.mean(0).float(), 1e-5, f"narrow fwd pro{pro} mean")
+
+
+@pytest.mark.parametrize("Cout,Kin,M,pro", [(32, 256, 32768, 2), (64, 64, 20000, 1), (128, 64, 9000, 1),
+                                            (64, 128, 5000, 0), (40, 200, 3000, 2), (32, 256, 100, 0)])
+def test_gemm_narrow_wgrad(K, dev, Cout, Kin, M, pro):
+    """Weight gradients of <= 64 output rows (64-row tiles, TM = 1) and/or <= 64 columns (TN = 1),
+    split-K over the points, with the wgrad prologues, vs float64; and the dgrad of the same layer
+    (TN = 1 when Kin <= 64)."""
+    g = torch.Generator().manual_seed(Cout + Kin + M)
+    dY = torch.randn(M, Cout, generator=g)
+    X = torch.randn(M, Kin, generator=g)
+    s, t = torch.rand(Kin, generator=g) + 0.5, torch.randn(Kin, generator=g)
+    dW = torch.empty(Cout, Kin, device=dev)
+    kw = {} if pro == 0 else dict(pro=pro, pro_s=s.to(dev), pro_t=t.to(dev))
+    K.wgrad(dY.to(dev), Cout, X.to(dev), Kin, Cout, Kin, M, dW, Kin, **kw)
+    Xp = X.double() if pro == 0 else (torch.relu(X.double() * s + t) if pro == 1 else torch.relu(X.double()) * s + t)
+    close(dW, dY.double().t() @ Xp, 1e-5, "narrow wgrad")
+    W = torch.randn(Cout, Kin, generator=g)
+    dX = torch.empty(M, Kin, device=dev)
+    K.gemm(M, Kin, Cout, dY.to(dev), Cout, W.to(dev), Kin, dX, Kin, b_kmajor=True)
+    close(dX, dY.double() @ W.double(), 1e-5, "narrow dgrad")
+
+
 CFG = {"source_latent_dim": 64, "target_latent_dim": 64, "sem_latent_dim": 16, "MAX_NUM_PARTS": 16}
 
 
