@@ -76,7 +76,11 @@ def variant_key(kw, M=None, N=None, K=None):
         if (epi == 0 and pa == 0 and pb == 0 and kw.get("A2") is None and not ak and K >= 512
                 and ((M + 127) // 128) * ((N + 127) // 128) <= 16):
             return None
-    return f"gemm2_kernel<{tf[ak]}, {tf[bk]}, {pa}, {pb}, {epi}>"
+    # block tile (csrc/mlp.hip launch()): 128 x 64 for <= 64 output columns, 64-row tiles for
+    # split-K / store GEMMs of <= 64 rows (the instance's last two template arguments TM, TN)
+    tn = 1 if N is not None and N <= 64 else 2
+    tm = 1 if M is not None and M <= 64 and epi in (0, 3) else 2
+    return f"gemm2_kernel<{tf[ak]}, {tf[bk]}, {pa}, {pb}, {epi}, {tm}, {tn}>"
 
 
 class DominantTimer:
