@@ -123,7 +123,8 @@ class GraphedStep:
         import torch.distributed as dist
         if not (getattr(self.inner, "collect", False) and dist.is_initialized() and dist.get_backend() == "nccl"):
             return False
-        return dist.get_world_size() == 1 or bool(self.inner.cfg.get("graph_inline_collectives", False))
+        flag = self.inner.cfg.get("graph_inline_collectives")     # None: by world size; True / False: forced
+        return dist.get_world_size() == 1 if flag is None else bool(flag)
 
     def _flat(self):
         """FlatAdam: the HIP layers write the gradients into its persistent flat buffer."""

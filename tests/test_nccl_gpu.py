@@ -11,6 +11,9 @@ split at the collectives). A one-rank all-reduce / all-gather is the identity, s
     losses match TrainStep to 1e-5 relative over the first three steps (a different fp32
     arithmetic path: Adam then amplifies the rounding differences of near-zero gradients, and
     the trajectories drift apart, ~1e-2 by the sixth step).
+The same two steps with cfg["graph_inline_collectives"] = False take the path world > 1 uses by
+default: segmented capture, the collectives run eagerly between graph segments on RCCL, the
+gradient all-reduce after the replay; they must equal the plain / eager steps bitwise too.
 Runs in a spawned process (its process group must not leak into the other tests)."""
 import os
 import socket
@@ -70,8 +73,6 @@ def _worker(port, q):
 
         cfg1 = dict(CFG, use_contrast_loss=0.0, cuda_graph=True)
         cfg2 = dict(CFG, cuda_graph=True, differentiable_gather=True)
-        # TrainStep references first: constructing a forced DataParallelStep switches the
-        # contrastive gather on process-wide
         ref1 = make(TrainStep, cfg1)
         l_ref1, p_ref1 = run(ref1), params(ref1)
         ref2 = make(TrainStep, cfg2)
@@ -93,6 +94,17 @@ def _worker(port, q):
         l_g2, p_g2 = run(g2), params(g2)
         res["graph2_eq_eager2"] = l_g2 == l_e2 and all(torch.equal(p_g2[k], p_e2[k]) for k in p_e2)
         res["contrast_rel"] = [abs(a - b) / abs(b) for a, b in zip(l_e2, l_ref2)]
+        # the world > 1 default: segmented capture, RCCL collectives eagerly between the graph
+        # segments and the gradient all-reduce after the replay (forced here at world size 1)
+        seg = {"graph_inline_collectives": False}
+        g3 = GraphedStep(make(DataParallelStep, dict(cfg1, **force, **seg)))
+        l_g3, p_g3 = run(g3), params(g3)
+        g4 = GraphedStep(make(DataParallelStep, dict(cfg2, **force, **seg)))
+        l_g4, p_g4 = run(g4), params(g4)
+        ent4 = next(iter(g4.graphs.values()))
+        res["segmented"] = not ent4[3] and len(ent4[1].graphs) == len(ent4[1].collectives) + 1 >= 2
+        res["seg1_eq_train"] = l_g3 == l_ref1 and all(torch.equal(p_g3[k], p_ref1[k]) for k in p_ref1)
+        res["seg2_eq_eager2"] = l_g4 == l_e2 and all(torch.equal(p_g4[k], p_e2[k]) for k in p_e2)
         res["losses"] = (l_ref1[:2], l_e1[:2], l_g1[:2])
         torch.cuda.synchronize()
     except Exception as e:
@@ -120,5 +132,8 @@ def test_nccl_world1_eager_and_captured(dev):
     assert r["graph1_eq_train"], r
     assert r["graph2_eq_eager2"], r
     assert max(r["contrast_rel"][:3]) <= 1e-5, r
+    assert r["segmented"], r                   # split at the all_gather: 2+ graphs, eager collectives
+    assert r["seg1_eq_train"], r
+    assert r["seg2_eq_eager2"], r
     print(f"\nnccl world 1: {r['buckets']} gradient buckets captured; contrast path rel dev per step "
           f"{['%.1e' % v for v in r['contrast_rel']]}")
