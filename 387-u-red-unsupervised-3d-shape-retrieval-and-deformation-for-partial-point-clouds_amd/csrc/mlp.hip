@@ -924,6 +924,18 @@ __device__ __forceinline__ float pro_lo(float x, float s, float t, float lo) {
     return x;
 }
 
+// Phase timing build (-DURED_GEMM_TIMING=1 -DURED_TS_M=.. -DURED_TS_N=.. -DURED_TS_K=..): the
+// BN-backward dgrad launches of that shape record, per workgroup, the real-time clock (100 MHz) at
+// start, first operand step ready, K-loop end and epilogue end, plus HW_ID / XCC_ID
+// (tools/gemm_phase.py reads them back through ured_debug_gemm_ts).
+#ifndef URED_GEMM_TIMING
+#define URED_GEMM_TIMING 0
+#endif
+#if URED_GEMM_TIMING
+constexpr int TS_SLOTS = 8192;
+__device__ unsigned long long ured_ts_buf[TS_SLOTS * 8];
+#endif
+
 // TM / TN: 32-row / 32-column MFMA tiles per wave (2 x 2 waves per block), so the block tile is
 // (64 TM) x (64 TN): 128 x 128 for the wide layers; TN = 1 (128 x 64) for outputs of <= 64
 // columns and TM = 1 (64 x ...) for split-K / store GEMMs of <= 64 output rows — the 32- and
@@ -962,6 +974,12 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
 
     // one output tile per block: tile blockIdx.x -> xcd_remap (blocks sharing an A panel on one XCD)
     if ((int)blockIdx.x >= ntiles) return;
+#if URED_GEMM_TIMING
+    const bool ts_on = EPI == URED_EPI_BNBWD && d.M == URED_TS_M && d.N == URED_TS_N && d.K == URED_TS_K &&
+                       blockIdx.x < TS_SLOTS;
+    unsigned long long ts_[4];
+    ts_[0] = __builtin_amdgcn_s_memrealtime();
+#endif
     int m0, n0;
     {
         const int tl = xcd_remap(blockIdx.x, ntiles);
@@ -1030,6 +1048,9 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         if (both && k0 == kbeg) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NPA + NPB) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
+#if URED_GEMM_TIMING
+        if (k0 == kbeg) ts_[1] = __builtin_amdgcn_s_memrealtime();
+#endif
         const float* As = smem + stage * 2 * TILE;
         const float* Bs = As + TILE;
         // next step's DMA goes into the other stage (its last readers passed the barrier
@@ -1147,7 +1168,24 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         stage ^= 1;
     }
 
+#if URED_GEMM_TIMING
+    ts_[2] = __builtin_amdgcn_s_memrealtime();
+#endif
     epilogue<EPI, true, TM, TN>(d, acc, m0, n0, red_f, red_i);
+#if URED_GEMM_TIMING
+    if (ts_on) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ts_[3] = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {
+            unsigned long long* o = ured_ts_buf + (size_t)blockIdx.x * 8;
+            o[0] = ts_[0]; o[1] = ts_[1]; o[2] = ts_[2]; o[3] = ts_[3];
+            o[4] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+            o[5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+            o[6] = (unsigned long long)m0 << 32 | (unsigned)n0;
+            o[7] = 1;
+        }
+    }
+#endif
 }
 
 // ---- small kernels -------------------------------------------------------------
@@ -2025,4 +2063,15 @@ int ured_group_colsum_split(const float* X, int ldx, int N, const int* off, int 
     return ured::launch_status("ured_group_colsum");
 }
 
+#if URED_GEMM_TIMING
+// phase-timing build only: copy the recorded workgroup timestamps out (n slots of 8 u64)
+int ured_debug_gemm_ts(unsigned long long* host, int n) {
+    if (n > TS_SLOTS) n = TS_SLOTS;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(ured_ts_buf), (size_t)n * 64) == hipSuccess ? 0 : -1;
+}
+int ured_debug_gemm_ts_clear() {
+    static unsigned long long z[TS_SLOTS * 8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(ured_ts_buf), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // extern "C"
