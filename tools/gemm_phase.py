@@ -25,6 +25,7 @@ def main():
     buf = (ctypes.c_ulonglong * (n * 8))()
     assert lib.ured_debug_gemm_ts(buf, n) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 8)
+    bid = np.nonzero(a[:, 7] == 1)[0]          # slot = blockIdx.x
     a = a[a[:, 7] == 1]
     if len(a) == 0:
         print("no workgroup recorded (shape not launched?)")
@@ -60,6 +61,17 @@ def main():
         conc.append(c2 / max(busy, 1e-9))
     print(f"  tiles per CU: min {min(ntile)} max {max(ntile)}; CU idle within the launch: mean "
           f"{np.mean(idle):.1f} us, max {np.max(idle):.1f}; time with 2 resident: {np.mean(conc):.2f}")
+    # placement: which block indices share a CU in the first round
+    first = t[:, 0] < 1.0
+    pairs = {}
+    for b, c in zip(bid[first], cu[first]):
+        pairs.setdefault(int(c), []).append(int(b))
+    ks = sorted(pairs)[:12]
+    print("  first-round blocks per CU (first 12 CUs):", [sorted(pairs[k]) for k in ks])
+    sec = [sorted(v)[1] - sorted(v)[0] for v in pairs.values() if len(v) == 2]
+    if sec:
+        print("  index distance between a CU's two first-round blocks: min %d max %d, most common %s" % (
+            min(sec), max(sec), np.bincount(np.array(sec) - min(sec)).argmax() + min(sec)))
     # start waves: how synchronous are the co-resident pairs
     order = np.argsort(t[:, 0])
     print("  first 8 starts (us):", np.round(t[order[:8], 0], 2).tolist())
