@@ -226,6 +226,29 @@ __host__ __device__ __forceinline__ size_t part_idx(int q, int col, int blk, int
 #define URED_DEBUG_BOUNDS 0
 #endif
 
+// Phase timing build (-DURED_GEMM_TIMING=1 -DURED_TS_M=.. -DURED_TS_N=.. -DURED_TS_K=..): the
+// BN-backward dgrad launches of that shape record, per workgroup, the real-time clock (100 MHz) at
+// start, first operand step ready, K-loop end and epilogue end, plus HW_ID / XCC_ID
+// (tools/gemm_phase.py reads them back through ured_debug_gemm_ts).
+#ifndef URED_GEMM_TIMING
+#define URED_GEMM_TIMING 0
+#endif
+#if URED_GEMM_TIMING
+constexpr int TS_SLOTS = 8192;
+__device__ unsigned long long ured_ts_buf[TS_SLOTS * 16];
+// slots per block: 0 start, 1 first K-step ready, 2 K-loop issued, 3 epilogue end (stores done),
+// 4 HW_ID, 5 XCC_ID, 6 tile, 7 valid, 8 Yp + column parameters landed, 9 G stores issued,
+// 10 column sums through LDS, 11 block partials written (wave 0's view; the last K-step's MFMAs
+// may still be executing at mark 2, so their drain shows up in the epilogue's first phases)
+__device__ __forceinline__ bool ts_shape(const UredGemmDesc& d) {
+    return d.M == URED_TS_M && d.N == URED_TS_N && d.K == URED_TS_K && blockIdx.x < TS_SLOTS;
+}
+#define URED_TS_MARK(d, k) do { if (ts_shape(d) && threadIdx.x == 0) \
+    ured_ts_buf[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define URED_TS_MARK(d, k) do { } while (0)
+#endif
+
 // ---- shared epilogue ---------------------------------------------------------
 // element (i, j, r): row = m0 + wm*64 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5), col = n0 + wn*64 + j*32 + (lane&31)
 #define RED(a, q, c) red_f[((a) * 2 + (q)) * BN + (c)]
@@ -348,6 +371,10 @@ __device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2]
         if (POOL) { pidx_[j] = d.pool_idx[(size_t)pg * d.N + col]; pgr_[j] = d.pool_grad[(size_t)pg * d.N + col]; }
     }
     pre();
+#if URED_GEMM_TIMING
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    URED_TS_MARK(d, 8);
+#endif
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const unsigned vo = r0 * lc + (unsigned)(n0 + wn * (32 * TN) + j * 32 + (lane & 31)) * 4u;
@@ -383,6 +410,7 @@ __device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2]
         a2 += __shfl_xor(a2, 32);
         s1[j] = a1; s2[j] = a2;
     }
+    URED_TS_MARK(d, 9);
 }
 
 template <int EPI, bool BUFST = false, int TM = 2, int TN = 2, class Pre = NoPre>
@@ -704,6 +732,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
             }
         }
         lds_barrier();
+        URED_TS_MARK(d, 10);
         if (wm == 0 && lane < 32) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
@@ -715,6 +744,7 @@ __device__ __forceinline__ void epilogue(const UredGemmDesc& d, f16v (&acc)[2][2
                 }
             }
         }
+        URED_TS_MARK(d, 11);
     }
 }
 #undef RED
@@ -923,18 +953,6 @@ __device__ __forceinline__ float pro_lo(float x, float s, float t, float lo) {
     if (PRO == URED_PRO_RES) return __builtin_fmaf(fmaxf(x, lo), s, t);
     return x;
 }
-
-// Phase timing build (-DURED_GEMM_TIMING=1 -DURED_TS_M=.. -DURED_TS_N=.. -DURED_TS_K=..): the
-// BN-backward dgrad launches of that shape record, per workgroup, the real-time clock (100 MHz) at
-// start, first operand step ready, K-loop end and epilogue end, plus HW_ID / XCC_ID
-// (tools/gemm_phase.py reads them back through ured_debug_gemm_ts).
-#ifndef URED_GEMM_TIMING
-#define URED_GEMM_TIMING 0
-#endif
-#if URED_GEMM_TIMING
-constexpr int TS_SLOTS = 8192;
-__device__ unsigned long long ured_ts_buf[TS_SLOTS * 8];
-#endif
 
 // TM / TN: 32-row / 32-column MFMA tiles per wave (2 x 2 waves per block), so the block tile is
 // (64 TM) x (64 TN): 128 x 128 for the wide layers; TN = 1 (128 x 64) for outputs of <= 64
@@ -1177,7 +1195,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ts_[3] = __builtin_amdgcn_s_memrealtime();
         if (threadIdx.x == 0) {
-            unsigned long long* o = ured_ts_buf + (size_t)blockIdx.x * 8;
+            unsigned long long* o = ured_ts_buf + (size_t)blockIdx.x * 16;
             o[0] = ts_[0]; o[1] = ts_[1]; o[2] = ts_[2]; o[3] = ts_[3];
             o[4] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
             o[5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
@@ -2064,13 +2082,13 @@ int ured_group_colsum_split(const float* X, int ldx, int N, const int* off, int 
 }
 
 #if URED_GEMM_TIMING
-// phase-timing build only: copy the recorded workgroup timestamps out (n slots of 8 u64)
+// phase-timing build only: copy the recorded workgroup timestamps out (n slots of 16 u64)
 int ured_debug_gemm_ts(unsigned long long* host, int n) {
     if (n > TS_SLOTS) n = TS_SLOTS;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(ured_ts_buf), (size_t)n * 64) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(ured_ts_buf), (size_t)n * 128) == hipSuccess ? 0 : -1;
 }
 int ured_debug_gemm_ts_clear() {
-    static unsigned long long z[TS_SLOTS * 8];
+    static unsigned long long z[TS_SLOTS * 16];
     return hipMemcpyToSymbol(HIP_SYMBOL(ured_ts_buf), z, sizeof z) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -22,9 +22,9 @@ def main():
     bench.main()
     lib = ctypes.CDLL(os.environ["URED_LIB"])
     n = 8192
-    buf = (ctypes.c_ulonglong * (n * 8))()
+    buf = (ctypes.c_ulonglong * (n * 16))()
     assert lib.ured_debug_gemm_ts(buf, n) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 8)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 16)
     bid = np.nonzero(a[:, 7] == 1)[0]          # slot = blockIdx.x
     a = a[a[:, 7] == 1]
     if len(a) == 0:
@@ -37,6 +37,13 @@ def main():
     xcc = a[:, 5].astype(np.int64) & 0xF
     cu = (xcc << 16) | (((hw >> 13) & 0x7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xF)
     ready, loop, epi = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2]
+    e = (a[:, 8:12].astype(np.int64) - t0) * 10e-3
+    if (a[:, 8] > 0).all():     # the full-tile BN-backward epilogue's marks
+        for name, v in (("epi: Yp + params landed", e[:, 0] - t[:, 2]), ("epi: compute + G stores", e[:, 1] - e[:, 0]),
+                        ("epi: column sums via LDS", e[:, 2] - e[:, 1]), ("epi: partials written", e[:, 3] - e[:, 2]),
+                        ("epi: store drain", t[:, 3] - e[:, 3])):
+            print(f"  {name:26s} mean {v.mean():7.2f}  p10 {np.percentile(v, 10):7.2f}  "
+                  f"p50 {np.percentile(v, 50):7.2f}  p90 {np.percentile(v, 90):7.2f} us")
     span = t[:, 3].max()
     print(f"workgroups {len(a)}  CUs {len(np.unique(cu))}  launch span {span:.1f} us")
     for name, v in (("start->first step ready", ready), ("K-loop", loop), ("epilogue", epi),
