@@ -116,8 +116,75 @@ __device__ __forceinline__ void load_chunk(const LaneSrc& sa, const LaneSrc& sb,
     ld16(sb, bkc, kb, K, false, b);
 }
 
+// partial tile -> LDS [wave][row][col]; element r: row (r&3) + 8(r>>2) + 4h, col li
+__device__ __forceinline__ void node_partial(float* red, const f16v& acc, int w, int h, int li) {
+    float* mine = red + w * NG_BM * NG_BN;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mine[((r & 3) + 8 * (r >> 2) + 4 * h) * NG_BN + li] = acc[r];
+}
+
+// 512 threads x 2 outputs: row t/16, columns 2(t%16), +1; the 8 waves' partial tiles summed in fixed
+// order, then bias, row-group bias, ReLU, gate, residual and accumulation
+__device__ __forceinline__ void node_combine(const UredNodeGemmDesc& d, const float* red, int m0, int n0) {
+    const int t = threadIdx.x;
+    const int row = t >> 4, cq = (t & 15) * 2;
+    const int m = m0 + row;
+    if (m >= d.M) return;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int col = cq + q, n = n0 + col;
+        if (n >= d.N) break;
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NG_WAVES; ++ww) v += red[ww * NG_BM * NG_BN + row * NG_BN + col];
+        if (d.bias) v += d.bias[n];
+        if (d.rowbias) v += d.rowbias[(long long)(m / d.rdiv) * d.ldrb + n];
+        if (d.relu_out) v = fmaxf(v, 0.f);
+        if (d.gate) v = d.gate[(long long)m * d.ldgate + n] > 0.f ? v : 0.f;
+        if (d.R && n < d.R_ncols) v += d.R[(long long)m * d.ldR + n];
+        float* cp = d.C + (long long)m * d.ldc + n;
+        if (d.accumulate) v += *cp;
+        *cp = v;
+    }
+}
+
+// bias gradient job: C[n] (+)= sum_m A(m, n)
+__device__ __forceinline__ void node_colsum(const UredNodeGemmDesc& d, int tile) {
+    __shared__ float part[16][33];
+    const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5, n = tile * 32 + cl;
+    float sacc = 0.f;
+    if (n < d.N) {
+        // unrolled so that eight loads are in flight per lane (the adds keep their order)
+        const float* col = d.A + (long long)n * d.sak;
+#pragma unroll 8
+        for (int m = rl; m < d.M; m += 16) sacc += col[(long long)m * d.sam];
+    }
+    part[rl][cl] = sacc;
+    __syncthreads();
+    if (rl == 0 && n < d.N) {
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v += part[q][cl];
+        d.C[n] = d.accumulate ? d.C[n] + v : v;
+    }
+}
+
 #ifndef URED_NODE_WG_PER_CU
 #define URED_NODE_WG_PER_CU 2
+#endif
+// Phase timing build (-DURED_NODE_TIMING=1 -DURED_NTS_M=.. -DURED_NTS_N=.. -DURED_NTS_K=..): launches
+// whose first job has that shape record per workgroup (wave 0) the real-time clock (100 MHz) at start,
+// first chunk landed, MFMA loop end, partial tiles in LDS, stores done (tools/node_phase.py reads
+// them through ured_debug_node_ts)
+#ifndef URED_NODE_TIMING
+#define URED_NODE_TIMING 0
+#endif
+#if URED_NODE_TIMING
+constexpr int NTS_SLOTS = 4096;
+__device__ unsigned long long ured_nts_buf[NTS_SLOTS * 8];
+#define URED_NTS(k) do { if (nts_on && threadIdx.x == 0) nts_[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define URED_NTS(k) do { } while (0)
 #endif
 // two workgroups per CU (the second launch-bounds argument is waves per SIMD: 4 -> <= 128 VGPRs;
 // one accumulator chain per wave, the four waves of a SIMD interleave their MFMAs), so a launch
@@ -131,29 +198,19 @@ __global__ __launch_bounds__(NG_NT, URED_NODE_WG_PER_CU * NG_WAVES / 4) void nod
     const NodeJob& J = jobs.job[ji];
     const UredNodeGemmDesc& d = J.d;
     const int tile = blockIdx.x - jobs.tile0[ji];
-    if (d.kind == URED_NODE_COLSUM) {         // bias gradient: C[n] (+)= sum_m A(m, n)
-        __shared__ float part[16][33];
-        const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5, n = tile * 32 + cl;
-        float sacc = 0.f;
-        if (n < d.N) {
-            // unrolled so that eight loads are in flight per lane (the adds keep their order)
-            const float* col = d.A + (long long)n * d.sak;
-#pragma unroll 8
-            for (int m = rl; m < d.M; m += 16) sacc += col[(long long)m * d.sam];
-        }
-        part[rl][cl] = sacc;
-        __syncthreads();
-        if (rl == 0 && n < d.N) {
-            float v = 0.f;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) v += part[q][cl];
-            d.C[n] = d.accumulate ? d.C[n] + v : v;
-        }
+    if (d.kind == URED_NODE_COLSUM) {
+        node_colsum(d, tile);
         return;
     }
     const int m0 = (tile / J.ntn) * NG_BM, n0 = (tile % J.ntn) * NG_BN;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63, h = lane >> 5, li = lane & 31;
     const bool akc = J.akc, bkc = J.bkc;
+#if URED_NODE_TIMING
+    const UredNodeGemmDesc& d0 = jobs.job[0].d;
+    const bool nts_on = d0.M == URED_NTS_M && d0.N == URED_NTS_N && d0.K == URED_NTS_K && blockIdx.x < NTS_SLOTS;
+    unsigned long long nts_[5] = {0, 0, 0, 0, 0};
+    URED_NTS(0);
+#endif
     // URED_NODE_WG_PER_CU 1: two accumulators (even / odd k-steps), independent MFMA chains
     // summed at the end; 2: one chain (registers for the second resident workgroup)
     constexpr bool TWO_ACC = URED_NODE_WG_PER_CU == 1;
@@ -167,6 +224,10 @@ __global__ __launch_bounds__(NG_NT, URED_NODE_WG_PER_CU * NG_WAVES / 4) void nod
     float a[16], b[16], an[16], bn[16];
     int c = w;
     if (c < nch) load_chunk(sa, sb, akc, bkc, c * NG_BK, h, d.K, a, b);
+#if URED_NODE_TIMING
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    URED_NTS(1);
+#endif
     while (c < nch) {
         const int cn = c + NG_WAVES;
         // one chunk of prefetch with one resident workgroup; with two, the other waves of the
@@ -190,31 +251,185 @@ __global__ __launch_bounds__(NG_NT, URED_NODE_WG_PER_CU * NG_WAVES / 4) void nod
         }
         c = cn;
     }
-    // partial tile -> LDS [wave][row][col]; element r: row (r&3) + 8(r>>2) + 4h, col li
-    float* mine = red + w * NG_BM * NG_BN;
+    URED_NTS(2);
+    f16v accs;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) mine[((r & 3) + 8 * (r >> 2) + 4 * h) * NG_BN + li] = TWO_ACC ? acc0[r] + acc1[r] : acc0[r];
+    for (int r = 0; r < 16; ++r) accs[r] = TWO_ACC ? acc0[r] + acc1[r] : acc0[r];
+    node_partial(red, accs, w, h, li);
     __syncthreads();
-    // 512 threads x 2 outputs: row t/16, columns 2(t%16), +1; waves summed in fixed order
-    const int row = t >> 4, cq = (t & 15) * 2;
-    const int m = m0 + row;
-    if (m >= d.M) return;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int col = cq + q, n = n0 + col;
-        if (n >= d.N) break;
-        float v = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < NG_WAVES; ++ww) v += red[ww * NG_BM * NG_BN + row * NG_BN + col];
-        if (d.bias) v += d.bias[n];
-        if (d.rowbias) v += d.rowbias[(long long)(m / d.rdiv) * d.ldrb + n];
-        if (d.relu_out) v = fmaxf(v, 0.f);
-        if (d.gate) v = d.gate[(long long)m * d.ldgate + n] > 0.f ? v : 0.f;
-        if (d.R && n < d.R_ncols) v += d.R[(long long)m * d.ldR + n];
-        float* cp = d.C + (long long)m * d.ldc + n;
-        if (d.accumulate) v += *cp;
-        *cp = v;
+    URED_NTS(3);
+#if URED_NODE_TIMING
+    if (nts_on && threadIdx.x == 0) {      // the end mark follows wave 0's stores
+        unsigned long long* o = ured_nts_buf + (size_t)blockIdx.x * 8;
+        o[0] = nts_[0]; o[1] = nts_[1]; o[2] = nts_[2]; o[3] = nts_[3];
+        o[5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        o[6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+        o[7] = 1;
     }
+#endif
+    node_combine(d, red, m0, n0);
+#if URED_NODE_TIMING
+    if (nts_on && threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ured_nts_buf[(size_t)blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+}
+
+// ---- v4: two K half-chunks in flight per wave --------------------------------------------------
+// v1 loads a wave's next K-chunk only after the current chunk's MFMAs, so a wave with c chunks
+// waits c dependent L2 round trips (tools/node_phase.py: 2.8 us to the first chunk, 3.4 more for the
+// second at 288 x 1536 x 512). v4 keeps URED_NODE_RING half-chunks (16 k per lane pair) in flight:
+// the loads of half q + RING are issued behind the MFMAs of half q, in ring order (sched_barrier), and past
+// the wave's last half it reloads chunk 0 (never consumed), so every iteration issues the same loads
+// and hipcc's wait counts stay exact. Operands are read as raw buffer loads (per-lane byte offset in
+// the VGPR offset, k * stride in the scalar offset); a k-contiguous operand (akc / bkc) as two 16-B
+// loads per half, any other as eight 4-B loads — the four combinations are separate loop bodies, so
+// each has a fixed load count. Same chunk -> wave assignment, MFMA order and fixed-order combine as
+// v1: bitwise v1. Jobs need K, k1 (A2 split) and n1 (B2 split) multiples of 32 and every element
+// below 2^29 of its operand base (node_v4_ok); other launches run v1.
+#ifndef URED_NODE_V4
+#define URED_NODE_V4 1
+#endif
+// half-chunks in flight per wave (3 at most for two strided operands: 16 loads per half). 2: DeformNet
+// fwd+bwd 1.228 ms graph-replayed vs v1 1.276; 4: 1.352 (profiles/r5w_node_v4.log)
+#ifndef URED_NODE_RING
+#define URED_NODE_RING 2
+#endif
+
+struct Src4 {
+    const float* base;   // operand base (uniform)
+    unsigned vo;         // this lane's byte offset: row / column offset + its lane half's 16 k
+    int sk4;             // k stride in bytes (4 for a k-contiguous operand)
+};
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// k = kb .. kb + 7 of this lane (kb uniform)
+template <bool KC>
+__device__ __forceinline__ void ld8(const Src4& s, int kb, float* out) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(s.base), (short)0,
+                                                                        0x7FFFFFFF, 0x00020000);
+    if constexpr (KC) {
+        const f4v x = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, s.vo, kb * 4, 0));
+        const f4v y = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, s.vo, kb * 4 + 16, 0));
+        out[0] = x[0]; out[1] = x[1]; out[2] = x[2]; out[3] = x[3];
+        out[4] = y[0]; out[5] = y[1]; out[6] = y[2]; out[7] = y[3];
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            out[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, s.vo, (kb + j) * s.sk4, 0));
+    }
+}
+
+// DEPTH half-chunks in flight (slot s holds halves s, s + DEPTH, ...); the MFMAs of a slot past
+// the wave's last half are skipped by a uniform branch with no loads inside (exact wait counts)
+template <bool AKC, bool BKC, int DEPTH>
+__device__ __forceinline__ void node_ring(const UredNodeGemmDesc& d, const Src4& a1, const Src4& a2, const Src4& bs,
+                                          int w, f16v& acc) {
+    const int nch = d.K / NG_BK;
+    const int mine = w < nch ? (nch - w + NG_WAVES - 1) / NG_WAVES : 0;   // chunks w, w+8, ...
+    const int halves = 2 * mine;
+    float a[DEPTH][8], b[DEPTH][8];
+    // half q: MFMAs j = 8(q & 1) .. +7 of chunk w + 8(q >> 1), i.e. k = c0 + 16h + 8(q & 1) + jj
+    auto load = [&](int slot, int q) {
+        const int c0 = (q < halves ? w + NG_WAVES * (q >> 1) : 0) * NG_BK, kh = 8 * (q & 1);
+        const bool first = c0 < d.k1;          // k1 % 32 == 0: a chunk lies in one A source
+        Src4 sa;
+        sa.base = first ? a1.base : a2.base;
+        sa.vo = first ? a1.vo : a2.vo;
+        sa.sk4 = first ? a1.sk4 : a2.sk4;
+        ld8<AKC>(sa, (first ? c0 : c0 - d.k1) + kh, a[slot]);
+        ld8<BKC>(bs, c0 + kh, b[slot]);
+    };
+#pragma unroll
+    for (int sl = 0; sl < DEPTH; ++sl) {
+        load(sl, sl);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    for (int q = 0; q < halves; q += DEPTH) {
+#pragma unroll
+        for (int sl = 0; sl < DEPTH; ++sl) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (sl == 0 || q + sl < halves) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[sl][j], b[sl][j], acc, 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            load(sl, q + sl + DEPTH);
+        }
+    }
+}
+
+__global__ __launch_bounds__(NG_NT, URED_NODE_WG_PER_CU * NG_WAVES / 4) void node_gemm4_kernel(const NodeJobs jobs) {
+    __shared__ float red[NG_WAVES * NG_BM * NG_BN];
+    int ji = 0;
+#pragma unroll
+    for (int q = 1; q < NG_JOBS; ++q)
+        if (q < jobs.njobs && (int)blockIdx.x >= jobs.tile0[q]) ji = q;
+    const NodeJob& J = jobs.job[ji];
+    const UredNodeGemmDesc& d = J.d;
+    const int tile = blockIdx.x - jobs.tile0[ji];
+    if (d.kind == URED_NODE_COLSUM) {
+        node_colsum(d, tile);
+        return;
+    }
+    const int m0 = (tile / J.ntn) * NG_BM, n0 = (tile % J.ntn) * NG_BN;
+    // the wave index as a provably uniform (SGPR) value: chunk counts and k offsets stay scalar
+    const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63, h = lane >> 5, li = lane & 31;
+    // rows / columns past M / N read the tile's first row / column (their outputs are never stored)
+    const long long mc = m0 + li < d.M ? m0 + li : m0;
+    const long long nc = n0 + li < d.N ? n0 + li : n0;
+    Src4 a1, a2, bs;
+    a1.base = d.A ? d.A : d.A2;                // k1 <= 0: every chunk reads A2
+    a1.sk4 = (int)(d.sak * 4);
+    a1.vo = (unsigned)((mc * d.sam + 16LL * h * d.sak) * 4);
+    if (d.A2) {
+        a2.base = d.A2; a2.sk4 = (int)(d.sak2 * 4);
+        a2.vo = (unsigned)((mc * d.sam2 + 16LL * h * d.sak2) * 4);
+    } else {
+        a2 = a1;
+    }
+    const bool b2 = d.B2 && n0 >= d.n1;        // n1 % 32 == 0: a 32-column tile lies in one B source
+    bs.base = b2 ? d.B2 : d.B;
+    const long long sbk = b2 ? d.sbk2 : d.sbk;
+    bs.sk4 = (int)(sbk * 4);
+    bs.vo = (unsigned)(((b2 ? (nc - d.n1) * d.sbn2 : nc * d.sbn) + 16LL * h * sbk) * 4);
+#if URED_NODE_TIMING
+    const UredNodeGemmDesc& d0 = jobs.job[0].d;
+    const bool nts_on = d0.M == URED_NTS_M && d0.N == URED_NTS_N && d0.K == URED_NTS_K && blockIdx.x < NTS_SLOTS;
+    unsigned long long nts_[5] = {0, 0, 0, 0, 0};
+    URED_NTS(0);
+    nts_[1] = nts_[0];                         // no separate first-chunk mark in the ring
+#endif
+    f16v acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // ring depth: at most ~48 loads in flight per wave (the vmcnt counter holds 63)
+    switch (J.akc * 2 + J.bkc) {
+        case 3: node_ring<true, true, URED_NODE_RING>(d, a1, a2, bs, w, acc); break;
+        case 2: node_ring<true, false, URED_NODE_RING>(d, a1, a2, bs, w, acc); break;
+        case 1: node_ring<false, true, URED_NODE_RING>(d, a1, a2, bs, w, acc); break;
+        default: node_ring<false, false, (URED_NODE_RING < 3 ? URED_NODE_RING : 3)>(d, a1, a2, bs, w, acc); break;
+    }
+    URED_NTS(2);
+    node_partial(red, acc, w, h, li);
+    __syncthreads();
+    URED_NTS(3);
+#if URED_NODE_TIMING
+    if (nts_on && threadIdx.x == 0) {
+        unsigned long long* o = ured_nts_buf + (size_t)blockIdx.x * 8;
+        o[0] = nts_[0]; o[1] = nts_[1]; o[2] = nts_[2]; o[3] = nts_[3];
+        o[7] = 1;
+    }
+#endif
+    node_combine(d, red, m0, n0);
+#if URED_NODE_TIMING
+    if (nts_on && threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ured_nts_buf[(size_t)blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 // ---- BatchNorm1d over node sets (rows [off[s], off[s+1]) form one call of the module) -------
@@ -400,6 +615,20 @@ static int check_node_job(const UredNodeGemmDesc& d, NodeJob& J) {
     return 0;
 }
 
+// v4 takes a job when its K, k1 (A2 split) and n1 (B2 split) are multiples of the 32-wide chunk /
+// tile and every element it reads lies below 2^29 elements of its operand base (31-bit byte
+// offsets in the buffer descriptors)
+static bool node_v4_ok(const UredNodeGemmDesc& d) {
+    if (d.kind == URED_NODE_COLSUM) return true;
+    const auto fits = [](long long v) { return v >= 0 && v < (1LL << 29); };
+    const int k1 = d.A2 ? (d.k1 < 0 ? 0 : d.k1) : d.K;
+    return d.K > 0 && d.K % NG_BK == 0 && (k1 >= d.K || k1 % NG_BK == 0) && (!d.B2 || d.n1 % NG_BN == 0) &&
+           (k1 == 0 || fits((long long)(d.M - 1) * d.sam + (long long)(k1 - 1) * d.sak)) &&
+           (!d.A2 || k1 >= d.K || fits((long long)(d.M - 1) * d.sam2 + (long long)(d.K - k1 - 1) * d.sak2)) &&
+           fits((long long)((d.B2 ? d.n1 : d.N) - 1) * d.sbn + (long long)(d.K - 1) * d.sbk) &&
+           (!d.B2 || fits((long long)(d.N - d.n1 - 1) * d.sbn2 + (long long)(d.K - 1) * d.sbk2));
+}
+
 int ured_node_gemm_batch(const UredNodeGemmDesc* const* ds, int n, void* stream) {
     ured::clear_error();
     URED_REQUIRE(ds && n >= 1 && n <= URED_NODE_MAX_JOBS, "ured_node_gemm_batch: 1..%d jobs", URED_NODE_MAX_JOBS);
@@ -419,7 +648,10 @@ int ured_node_gemm_batch(const UredNodeGemmDesc* const* ds, int n, void* stream)
     }
     if (jobs.njobs == 0) return 0;
     for (int q = jobs.njobs; q <= NG_JOBS; ++q) jobs.tile0[q] = tiles;
-    hipLaunchKernelGGL(node_gemm_kernel, dim3(tiles), dim3(NG_NT), 0, (hipStream_t)stream, jobs);
+    bool v4 = URED_NODE_V4;
+    for (int q = 0; q < jobs.njobs; ++q) v4 = v4 && node_v4_ok(jobs.job[q].d);
+    if (v4) hipLaunchKernelGGL(node_gemm4_kernel, dim3(tiles), dim3(NG_NT), 0, (hipStream_t)stream, jobs);
+    else hipLaunchKernelGGL(node_gemm_kernel, dim3(tiles), dim3(NG_NT), 0, (hipStream_t)stream, jobs);
     return ured::launch_status("ured_node_gemm");
 }
 
@@ -457,4 +689,11 @@ int ured_node_bn_bwd(const UredNodeBNBwdDesc* dp, void* stream) {
     return ured::launch_status("ured_node_bn_bwd");
 }
 
+#if URED_NODE_TIMING
+// phase-timing build only: copy the recorded node-GEMM workgroup timestamps out (n slots of 8 u64)
+int ured_debug_node_ts(unsigned long long* host, int n) {
+    if (n > NTS_SLOTS) n = NTS_SLOTS;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(ured_nts_buf), (size_t)n * 64) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // extern "C"
