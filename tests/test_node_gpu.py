@@ -151,6 +151,44 @@ def test_batched_jobs_equal_single_launches(dev):
     _close(outs_b[3], gw.double().t() @ xw.double())
 
 
+def test_v4_equals_v1_bitwise(dev):
+    """csrc/node.hip runs a launch on the v4 kernel (two half-chunks in flight, buffer loads) when
+    every job has K, k1, n1 multiples of 32, else on v1. A job with K = 45 in the batch forces v1
+    for all of them; the same jobs launched one by one take v4: same chunk -> wave assignment, MFMA
+    order and combine, so bitwise the same, for every operand-layout combination (k-contiguous /
+    strided A and B), a split A (k1 = 64) and accumulation."""
+    from ured_hip import node
+    g = torch.Generator().manual_seed(11)
+    mk = lambda *s: torch.randn(*s, generator=g).to(dev)   # noqa: E731
+    x, W = mk(288, 1536), mk(512, 1536)          # A, B k-contiguous (forward)
+    gr, Wd = mk(288, 1024), mk(1024, 512)        # A k-contiguous, B strided (dgrad)
+    gw, xw = mk(288, 256), mk(288, 96)           # A, B strided (wgrad)
+    xs, ms, Ws = mk(64, 64), mk(64, 96), mk(128, 160)   # split A (k1 = 64)
+    xo, Wo = mk(40, 45), mk(20, 45)              # K = 45: v1 only
+    c0 = mk(256, 96)                             # accumulated into by the wgrad job
+
+    def jobs(o):
+        o[3].copy_(c0)
+        return [node.linear_desc(x, W, o[0]), node.dgrad_desc(gr, Wd, o[1]),
+                node.node_gemm_desc(64, 128, 160, xs.data_ptr(), xs.stride(0), 1, Ws.data_ptr(), 1, Ws.stride(0),
+                                    o[2], 128, A2=ms.data_ptr(), sam2=ms.stride(0), sak2=1, k1=64),
+                node.wgrad_desc(gw, xw, o[3], accumulate=True),
+                node.linear_desc(xo, Wo, o[4])]
+
+    shapes = [(288, 512), (288, 512), (64, 128), (256, 96), (40, 20)]
+    ob = [torch.empty(*s, device=dev) for s in shapes]
+    os_ = [torch.empty(*s, device=dev) for s in shapes]
+    node.launch(*jobs(ob))                       # v1 (the K = 45 job)
+    for d in jobs(os_):
+        node.launch(d)                           # v4 for all but the last
+    for i in range(5):
+        assert torch.equal(ob[i], os_[i]), i
+    _close(ob[0], x.double() @ W.double().t())
+    _close(ob[1], gr.double() @ Wd.double())
+    _close(ob[2], torch.cat([xs, ms], 1).double() @ Ws.double().t())
+    _close(ob[3], gw.double().t() @ xw.double() + c0.double())
+
+
 @pytest.mark.parametrize("sets", [(0, 32, 288), (0, 32)])
 def test_node_ffn_and_linear2_match_reference(dev, sets):
     """ResidualAttentionMessagePropagation's FFN update out = x + conv2(BN(relu(conv1(cat([x, m])))))
