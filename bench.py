@@ -558,8 +558,11 @@ def dry_run(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 50 timed steps after 8 warmup steps (the 4 batches' graphs captured, then each replayed once):
+    # the steady-state rate; a 10-step window right after the captures read 2 % low
+    # (profiles/r5s_bench_window.log)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--points", type=int, default=2048)
     ap.add_argument("--parts", type=int, default=4)
