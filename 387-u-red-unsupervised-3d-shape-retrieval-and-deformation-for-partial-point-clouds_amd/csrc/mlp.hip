@@ -850,10 +850,6 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // k >= K row of a k-major operand: the hardware returns zeros for them.
 constexpr unsigned BUF_OOB = 0x80000000u;
 constexpr int PRO_LDS = 1024;            // max prologue channels staged in LDS by gemm2
-// the A / B prologue of each k-slice pinned in between the MFMAs (sched_group_barrier)
-#ifndef URED_GEMM_INTERLEAVE
-#define URED_GEMM_INTERLEAVE 1
-#endif
 // 64-wide block tiles for the narrow layers (gemm2_kernel TM / TN); 0 = 128 x 128 everywhere
 #ifndef URED_GEMM_NARROW
 #define URED_GEMM_NARROW 1
@@ -877,7 +873,6 @@ __host__ __device__ inline bool buf_ok(const UredGemmDesc& d) {
 struct BufOperand {
     __amdgpu_buffer_rsrc_t rs;   // raw buffer descriptor: base, stride 0, num_records (bytes)
     unsigned vo[4];              // per-lane byte offsets of the wave's pieces
-    int ko[4];                   // row-major image: k offset of the lane's 4-element chunk in the step
 };
 
 // NP = EXT / 32: 16-B chunks per wave-lane of an EXT-wide operand image (EXT = 128 or 64 rows /
@@ -896,7 +891,6 @@ __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld,
             const int r = c >> 3, p = c & 7, sl = p ^ ((r >> 1) & 7);
             const int row = e0 + r;
             o.vo[i] = row < ext ? (unsigned)(((long long)row * ld + 4 * sl) * 4) : BUF_OOB;
-            o.ko[i] = 4 * sl;
         } else {
             const int kk = c / CPR, c4 = c % CPR;
             const int col = e0 + 4 * c4;
@@ -917,40 +911,23 @@ __device__ __forceinline__ void buf_setup(BufOperand& o, const float* G, int ld,
 constexpr unsigned GEMM2_SMEM_BYTES = 2u * 2u * (unsigned)(BM * BK) * 4u;   // both stages, A|B images
 
 // One wave's NP 1-KB pieces of an operand image. smem: the stage images' LDS object; off:
-// wave-uniform byte offset of this wave's first piece inside it. A step that runs past the
-// reduction's end (tail, wave-uniform) zero-fills the k >= kend chunks of a row-major image (its
-// rows are contiguous in k, so those chunks would read the next row); a k-major image's rows past
-// kend lie past num_records already. Zeros in both operands' k >= kend parts make the MFMAs of
-// those k add exact zeros whatever the prologues make of them.
+// wave-uniform byte offset of this wave's first piece inside it.
 template <bool KM, int NP>
-__device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, float* smem, unsigned off,
-                                         bool tail, int kend) {
+__device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, float* smem, unsigned off) {
     const unsigned toff = KM ? (unsigned)k0 * (unsigned)ld * 4u : (unsigned)k0 * 4u;
 #if URED_DEBUG_BOUNDS
     if (off + NP * 1024u > GEMM2_SMEM_BYTES || (off & 1023u)) __builtin_trap();
 #endif
     char* base = reinterpret_cast<char*>(smem) + off;
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-        unsigned v = o.vo[i] + toff;
-        if (!KM && tail) v = k0 + o.ko[i] < kend ? v : BUF_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(o.rs, (lds_void_t*)(base + i * 1024), 16, v, 0, 0, 0);
-    }
+    for (int i = 0; i < NP; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(o.rs, (lds_void_t*)(base + i * 1024), 16, o.vo[i] + toff, 0, 0, 0);
 }
 
 template <int PRO>
 __device__ __forceinline__ float pro_v(float x, float s, float t) {
     if (PRO == URED_PRO_ENC) return fmaxf(__builtin_fmaf(x, s, t), 0.f);
     if (PRO == URED_PRO_RES) return __builtin_fmaf(fmaxf(x, 0.f), s, t);
-    return x;
-}
-
-// pro_v with the ReLU clamp as an operand: lo = 0 is pro_v, lo = -inf with s = 1, t = 0 the
-// identity (the raw steps of a concatenated A)
-template <int PRO>
-__device__ __forceinline__ float pro_lo(float x, float s, float t, float lo) {
-    if (PRO == URED_PRO_ENC) return fmaxf(__builtin_fmaf(x, s, t), lo);
-    if (PRO == URED_PRO_RES) return __builtin_fmaf(fmaxf(x, lo), s, t);
     return x;
 }
 
@@ -974,10 +951,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     __shared__ __attribute__((aligned(16))) float smem[2 * 2 * TILE];
     __shared__ float red_f[4 * BN];
     __shared__ int red_i[4 * BN];
-    // scale [0, PRO_LDS) | 16 ones | shift [PSH, PSH + PRO_LDS) | 16 zeros: the raw (k >= k1) steps
-    // of a concatenated A read the identity rows, so every K-step runs the same branch-free prologue
-    constexpr int PSH = PRO_LDS + 16;
-    __shared__ __attribute__((aligned(16))) float pro_lds[PRO_IN_LDS ? 2 * PSH : 4];
+    __shared__ __attribute__((aligned(16))) float pro_lds[PRO_IN_LDS ? 2 * PRO_LDS : 4];   // scale | shift
 
     const int ntm = (d.M + BMT - 1) / BMT, ntn = (d.N + BNT - 1) / BNT;
     const int ntiles = ntm * ntn;
@@ -1019,17 +993,15 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
     const unsigned lds_a = wu * (NPA * 1024u), lds_b = TILE * 4u + wu * (NPB * 1024u);
     auto issue_a = [&](int stage, int k0) {
         const unsigned la = lds_a + (unsigned)stage * (2u * TILE * 4u);
-        const bool tl = k0 + BK > kend;
-        if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false, NPA>(ba2, d.lda2, k0 - d.k1, smem, la, tl, kend - d.k1);
-        else buf_tile<A_KM, NPA>(ba, d.lda, k0, smem, la, tl, kend);
+        if (!A_KM && has_a2 && k0 >= d.k1) buf_tile<false, NPA>(ba2, d.lda2, k0 - d.k1, smem, la);
+        else buf_tile<A_KM, NPA>(ba, d.lda, k0, smem, la);
     };
     auto issue_b = [&](int stage, int k0) {
-        buf_tile<B_KM, NPB>(bb, d.ldb, k0, smem, lds_b + (unsigned)stage * (2u * TILE * 4u), k0 + BK > kend, kend);
+        buf_tile<B_KM, NPB>(bb, d.ldb, k0, smem, lds_b + (unsigned)stage * (2u * TILE * 4u));
     };
 
     if constexpr (PRO_IN_LDS) {   // visible after the first loop barrier
-        for (int i = t; i < d.k1; i += NT) { pro_lds[i] = d.pro_s[i]; pro_lds[PSH + i] = d.pro_t[i]; }
-        if (t < 16) { pro_lds[PRO_LDS + t] = 1.f; pro_lds[PSH + PRO_LDS + t] = 0.f; }
+        for (int i = t; i < d.k1; i += NT) { pro_lds[i] = d.pro_s[i]; pro_lds[PRO_LDS + i] = d.pro_t[i]; }
     }
     int stage = 0;
     // a reduction of exactly two K-steps (the 64-channel layers' K = 64) gets both stages'
@@ -1071,6 +1043,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
 #endif
         const float* As = smem + stage * 2 * TILE;
         const float* Bs = As + TILE;
+        const bool tail = k0 + BK > kend;
         // next step's DMA goes into the other stage (its last readers passed the barrier
         // above); URED_DMA_SPREAD picks the issue point (see its definition)
         const bool next = k0 + BK < kend && !both;
@@ -1080,18 +1053,15 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
         // prologue (and the MFMAs behind it) can start on the first A fragments
         float ss[16], tt[16];
         // k1 (start of the raw concatenated A2) is a multiple of BK when A2 is present
-        // (buf_ok), so "this K-step needs the prologue" is wave-uniform
+        // (buf_ok), so "this K-step needs the prologue" is wave-uniform: a scalar branch
+        // instead of a per-element select
         const bool pro_step = PRO_IN_LDS && k0 < d.k1;
-        // the clamp of the prologue's ReLU: 0 on prologue steps, -inf (none) on raw steps, which
-        // also read scale 1 / shift 0 — one instruction sequence for both (no branch, so the
-        // scheduler can interleave the prologue with the MFMAs that consume it)
-        const float plo = pro_step ? 0.f : -__builtin_inff();
-        if constexpr (PRO_IN_LDS) {
-            const int kc = pro_step ? min(k0 + 16 * h, d.k1 - 16) : PRO_LDS;
+        if (pro_step) {
+            const int kc = min(k0 + 16 * h, d.k1 - 16);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float4 sv = *reinterpret_cast<const float4*>(pro_lds + kc + 4 * q);
-                const float4 tv = *reinterpret_cast<const float4*>(pro_lds + PSH + kc + 4 * q);
+                const float4 tv = *reinterpret_cast<const float4*>(pro_lds + PRO_LDS + kc + 4 * q);
                 ss[4 * q] = sv.x; ss[4 * q + 1] = sv.y; ss[4 * q + 2] = sv.z; ss[4 * q + 3] = sv.w;
                 tt[4 * q] = tv.x; tt[4 * q + 1] = tv.y; tt[4 * q + 2] = tv.z; tt[4 * q + 3] = tv.w;
             }
@@ -1136,31 +1106,40 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
             issue_b(stage ^ 1, k0 + BK);
             __builtin_amdgcn_sched_barrier(0);
         }
-        // ---- prologues (previous layer's BN+ReLU), the K tail, MFMAs. The prologue of k-slice j is
-        // computed right before the MFMAs that consume it (URED_GEMM_INTERLEAVE: sched_group_barrier
-        // pins VALU j, MFMA j, VALU j+1, ...), so its fma/max pairs co-issue under the previous
-        // MFMAs instead of running as one VALU burst in front of the first. (A tail step's k >= K
-        // parts are zero in both operand images: buf_tile.)
-        // s_setprio(1) around the cluster keeps hipcc from moving MFMAs out of it, in among the next
-        // step's loads (cdna_hip_programming.md T5): forward, wgrad and store variants +1-2 %
-        // isolated (tools/ab_libs_step.sh, same box, two rounds); the BN-backward dgrad went
-        // -1..+1 %, so it keeps the plain schedule
+        // ---- prologues (previous layer's BN+ReLU) and the K tail, on the fragments
+        if constexpr (!A_KM && PRO_A != URED_PRO_NONE) {
+            if (pro_step) {
+                // scalar v_fma_f32 + v_max_f32: beside MFMAs a packed v_pk_fma_f32 costs more
+                // issue time than two plain fmas (MI355X_MICROARCH.md, filler prices)
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) a[tm][j] = pro_v<PRO_A>(a[tm][j], ss[j], tt[j]);
+            }
+        }
+        if constexpr (B_KM && PRO_B != URED_PRO_NONE) {
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) b[tn][j] = pro_v<PRO_B>(b[tn][j], bs_[tn], bt_[tn]);
+        }
+        if (tail) {   // zero the k >= K part of the reduction (the images hold clamped copies)
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) a[tm][j] = (k0 + 16 * h + j < kend) ? a[tm][j] : 0.f;
+        }
+        // ---- MFMAs. s_setprio(1) around the cluster keeps hipcc from moving MFMAs out of it, in
+        // among the next step's loads (cdna_hip_programming.md T5): forward, wgrad and store
+        // variants +1-2 % isolated (tools/ab_libs_step.sh, same box, two rounds); the BN-backward
+        // dgrad went -1..+1 %, so it keeps the plain schedule
         constexpr bool PRIO = EPI != URED_EPI_BNBWD;
-        constexpr bool APRO = !A_KM && PRO_A != URED_PRO_NONE, BPRO = B_KM && PRO_B != URED_PRO_NONE;
         // URED_DMA_SPREAD == 1: MFMA group (of 16) behind which the next step's A / B halves are
         // issued: 6 / 11 with a k-major B, 1 / 5 with a row-major B (profiles/r4zh_*)
         constexpr int DMA_JA = B_KM ? 6 : 1, DMA_JB = B_KM ? 11 : 5;
-        auto slice = [&](int j) {
-            if constexpr (APRO) {
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-                for (int tm = 0; tm < TM; ++tm) a[tm][j] = pro_lo<PRO_A>(a[tm][j], ss[j], tt[j], plo);
-            }
-            if constexpr (BPRO) {
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) b[tn][j] = pro_v<PRO_B>(b[tn][j], bs_[tn], bt_[tn]);
-            }
-        };
-        auto mfmas = [&](int j) {
+        for (int j = 0; j < 16; ++j) {
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -1168,20 +1147,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
                     acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[tm][j], b[tn][j], acc[tm][tn], 0, 0, 0);
             if (URED_DMA_SPREAD == 1 && next && j == DMA_JA) issue_a(stage ^ 1, k0 + BK);
             if (URED_DMA_SPREAD == 1 && next && j == DMA_JB) issue_b(stage ^ 1, k0 + BK);
-        };
-        if (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) { slice(j); mfmas(j); }
-#if URED_GEMM_INTERLEAVE
-        if constexpr (APRO || BPRO) {
-            constexpr int NV = (APRO ? 2 * TM : 0) + (BPRO ? 2 * TN : 0);   // fma + max per operand
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);          // VALU
-                __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);     // MFMA
-            }
         }
-#endif
         if (PRIO) __builtin_amdgcn_s_setprio(0);
         stage ^= 1;
     }
