@@ -621,7 +621,9 @@ static int check_node_job(const UredNodeGemmDesc& d, NodeJob& J) {
 static bool node_v4_ok(const UredNodeGemmDesc& d) {
     if (d.kind == URED_NODE_COLSUM) return true;
     const auto fits = [](long long v) { return v >= 0 && v < (1LL << 29); };
-    const int k1 = d.A2 ? (d.k1 < 0 ? 0 : d.k1) : d.K;
+    // v4 reads A2 at element (k - k1): a negative k1 would read past the bound checked below
+    if (d.A2 && d.k1 < 0) return false;
+    const int k1 = d.A2 ? d.k1 : d.K;
     return d.K > 0 && d.K % NG_BK == 0 && (k1 >= d.K || k1 % NG_BK == 0) && (!d.B2 || d.n1 % NG_BN == 0) &&
            (k1 == 0 || fits((long long)(d.M - 1) * d.sam + (long long)(k1 - 1) * d.sak)) &&
            (!d.A2 || k1 >= d.K || fits((long long)(d.M - 1) * d.sam2 + (long long)(d.K - k1 - 1) * d.sak2)) &&

@@ -104,7 +104,8 @@ class GraphedStep:
         return bool(cfg["use_residuals_reg"] > 0.0 and epoch > cfg["init_p_m_loss"])
 
     def key(self, batch, epoch=0):
-        uq = batch.get("src_unique")
+        # the step encodes every source slot when cfg["unique_sources"] is off (engine/train.py)
+        uq = batch.get("src_unique") if self.inner.cfg.get("unique_sources", True) else None
         pb = batch.get("part_bounds")          # sizes the loss head's NN launches (ured_hip/ops.py)
         return (None if uq is None else uq.U, self.gate(epoch), None if pb is None else pb.key())
 

@@ -63,13 +63,17 @@ class NNDenseFunction(Function):
         b, n, _ = xyz1.shape
         m = xyz2.shape[1]
         dev = xyz1.device
-        # the four outputs are views of ONE allocation (host cost of the reference-API call)
-        buf = torch.empty(2 * b * (n + m), device=dev, dtype=torch.float32)
-        dist1, dist2 = buf[:b * n].view(b, n), buf[b * n:b * (n + m)].view(b, m)
-        idx1 = buf[b * (n + m):b * (2 * n + m)].view(torch.int32).view(b, n)
-        idx2 = buf[b * (2 * n + m):].view(torch.int32).view(b, m)
+        # dist1 / dist2 are allocations of their own, as the reference's chamfer_3DDist returns
+        # them: a differentiable output that is a view made inside a custom Function rejects
+        # in-place ops (dist1.clamp_()). The non-differentiable indices share one allocation.
+        dist1 = torch.empty(b, n, device=dev, dtype=torch.float32)
+        dist2 = torch.empty(b, m, device=dev, dtype=torch.float32)
+        ibuf = torch.empty(b * (n + m), device=dev, dtype=torch.int32)
+        idx1, idx2 = ibuf[:b * n].view(b, n), ibuf[b * n:].view(b, m)
         if n == 0 or m == 0:
-            buf.zero_()
+            dist1.zero_()
+            dist2.zero_()
+            ibuf.zero_()
         else:
             ws, nbytes = _workspace(b, n, m, b * n, b * m, 3, dev)
             _lib.call("ured_nn_fwd_ws", _lib.ptr(xyz1), _lib.ptr(xyz2), b, n, m, 3,

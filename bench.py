@@ -686,22 +686,40 @@ def main():
     elapsed = float(t.item())
     loss_val = float(T["all_loss"].item())
 
-    def timed_rate(steps, bs=None):   # same protocol (barrier + sync both sides, max over ranks)
+    def timed_rate(steps, bs=None):
+        """A side workload under the headline's protocol: the same step mode (HIP-graph replay
+        unless --eager, each batch's graph captured and replayed once before timing, in a
+        GraphedStep of its own so the headline's graphs stay as they are), barrier + sync on both
+        sides, max over ranks. So a side rate differs from the headline by its workload alone."""
         bs = bs or batches
-        for i in range(2):
-            eager.step(bs[i % len(bs)])
+        runner = eager
+        warm = 2
+        if use_graph:
+            from engine.graph import GraphedStep
+            runner = GraphedStep(eager, max_graphs=len(bs))
+            warm = 2 * len(bs)
+        for i in range(warm):
+            runner.step(bs[i % len(bs)])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
         for i in range(steps):
-            eager.step(bs[i % len(bs)])
+            runner.step(bs[i % len(bs)])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         tt = torch.tensor([time.perf_counter() - t1], device=dev)
         if world > 1:
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        if runner is not eager:           # release the side workload's graphs and their pools
+            runner.graphs.clear()
+            runner.g_update = None
+            del runner
+            import gc
+            gc.collect()
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
         return steps * world / float(tt.item())
 
     all_slots_rate = None
@@ -717,7 +735,8 @@ def main():
     if not args.no_k16_rate and args.parts != 16:
         # SURVEY §8(d)'s stress case: 16 parts per target, no padding slots (~200 distinct sources)
         b16 = [batch_to_device(synthetic.make_batch(args.batch, args.points, db.num_sources, parts=16,
-                                                    seed=5000 + 1000 * rank + i), dev, db.num_sources)
+                                                    seed=5000 + 1000 * rank + i), dev, db.num_sources,
+                               bucket=args.graph_bucket if use_graph else None)
                for i in range(4)]
         k16_rate = timed_rate(args.steps, b16)
         del b16
@@ -823,6 +842,8 @@ def main():
         extra["all_slots_iters_s"] = round(all_slots_rate, 4)
     if k16_rate is not None:
         extra["k16_iters_s"] = round(k16_rate, 4)
+    if all_slots_rate is not None or k16_rate is not None:
+        extra["side_rates_mode"] = "hip_graph" if use_graph else "eager"
     if loader is not None:
         extra["loader_iters_s"] = loader["iters_s"]
         extra["loader"] = loader

@@ -78,6 +78,26 @@ def test_dense_bwd(unn, dev, b, n, m):
     assert torch.equal(a2.grad, a.grad)
 
 
+def test_dense_outputs_allow_inplace(unn, dev):
+    """dist1 / dist2 are independent allocations (as the reference's chamfer_3DDist returns them):
+    an in-place op on one of them works under autograd and leaves the other and the indices
+    untouched; the clamped gradient flows through the in-place op."""
+    p1, p2 = _rand((2, 300, 3), 41), _rand((2, 200, 3), 42)
+    a = torch.from_numpy(p1).to(dev).requires_grad_(True)
+    c = torch.from_numpy(p2).to(dev).requires_grad_(True)
+    d1, d2, i1, i2 = unn.nn_dense(a, c)
+    assert d1.data_ptr() != d2.data_ptr() and d1._base is None and d2._base is None
+    d2_before, i1_before = d2.detach().clone(), i1.clone()
+    d1.clamp_(max=0.001)
+    assert torch.equal(d2, d2_before) and torch.equal(i1, i1_before)
+    (d1.sum() + d2.sum()).backward()
+    r = nn_ref.nn_fwd(p1, p2)
+    g1 = (r[0] <= 0.001).astype(np.float32)
+    ga, gc = nn_ref.nn_bwd(p1, p2, g1, np.ones_like(r[1]), r[2], r[3])
+    np.testing.assert_allclose(a.grad.cpu().numpy(), ga, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(c.grad.cpu().numpy(), gc, rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("b,n,m", [(4, 100, 200), (2, 3000, 17), (1, 2048, 2048)])
 def test_dense_bwd_set_equals_accumulate(unn, dev, b, n, m):
     """ured_nn_bwd_set (written gradients, the autograd path) == ured_nn_bwd (accumulated into

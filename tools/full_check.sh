@@ -1,10 +1,10 @@
-# Round 5 full check on one box: the whole GPU suite once (-x, multi-process rehearsals last), smoke,
+# Full check on one box: the whole GPU suite once (-x, multi-process rehearsals last), smoke,
 # the default bench line, then a whole-step A/B of the DMA issue point (in-tree: ahead of the
 # MFMAs; B: among them).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-TAG=${TAG:-r5b}
+TAG=${TAG:-r6a}
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { echo "pytest failed rc=$?"; tail -40 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
 tail -3 gpurun_out/${TAG}_gpu_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/${TAG}_smoke.log; exit 1; }

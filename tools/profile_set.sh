@@ -1,7 +1,7 @@
-# Round 5 profile set of the current tree (the bench roofline's sources): kernel trace of the timed
-# replayed steps, FETCH/WRITE PMC passes, held clock and MFMA-busy passes. Usage: bash tools/r5_profile.sh <tag>
+# Profile set of the current tree (the bench roofline's sources): kernel trace of the timed
+# replayed steps, FETCH/WRITE PMC passes, held clock and MFMA-busy passes. Usage: bash tools/profile_set.sh <tag>
 set -o pipefail
-T=${1:-r5z}
+T=${1:-r6a}
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 bash tools/prof_step.sh $T 20 > gpurun_out/${T}_prof_step.log 2>&1 || { tail -20 gpurun_out/${T}_prof_step.log; exit 1; }
