@@ -113,6 +113,7 @@ __global__ __launch_bounds__(256) void emd_bid_kernel(const float* __restrict__ 
     }
     if (best_i < 0) { w.bid[base + i] = -1; return; }   // no finite value (cannot happen for finite inputs)
     const float incr = best - better + eps;
+    URED_DBG_CHECK(best_i < n);
     w.bid[base + i] = best_i;
     w.inc[base + i] = incr;
     const unsigned long long key = ((unsigned long long)__float_as_uint(incr) << 32) | (0xFFFFFFFFu - (unsigned)i);
@@ -127,11 +128,13 @@ __global__ __launch_bounds__(256) void emd_assign_kernel(int n, int* assignment,
     if (assignment[base + i] != -1) return;
     const int j = w.bid[base + i];
     if (j < 0) return;
+    URED_DBG_CHECK(j < n);
     const unsigned long long key = w.key[base + j];
     const bool won = last || (0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull)) == (unsigned)i;
     if (!won) return;
     if (!last) {
         const int prev = w.inv[base + j];
+        URED_DBG_CHECK(prev >= -1 && prev < n);
         if (prev != -1) assignment[base + prev] = -1;
         w.key[base + j] = 0ull;
     }
@@ -147,6 +150,7 @@ __global__ __launch_bounds__(256) void emd_dist_kernel(const float* __restrict__
     if (i >= n) return;
     const size_t base = (size_t)b * n;
     const int k = assignment[base + i];
+    URED_DBG_CHECK(k >= -1 && k < n);
     const float* p = xyz1 + 3 * (base + i);
     const float* r = xyz2 + 3 * (base + (k < 0 ? 0 : k));
     dist[base + i] = sqd(r[0], r[1], r[2], p[0], p[1], p[2]);   // (x1 - x2)^2 terms, emd_cuda.cu:247-250
@@ -160,6 +164,7 @@ __global__ __launch_bounds__(256) void emd_bwd_kernel(const float* __restrict__ 
     if (i >= n) return;
     const size_t base = (size_t)b * n;
     const int k = assignment[base + i];
+    URED_DBG_CHECK(k >= -1 && k < n);
     const float* p = xyz1 + 3 * (base + i);
     const float* r = xyz2 + 3 * (base + (k < 0 ? 0 : k));
     const float g = gd[base + i] * 2.f;

@@ -122,11 +122,14 @@ __global__ __launch_bounds__(LT) void cd_pair_prep_kernel(CdShape sh, const floa
         const int s = (int)(t / (sh.P + 1)), i = (int)(t % (sh.P + 1));
         const int h = s / sh.B, b = s % sh.B;
         const int kb = (int)k[b];
+        URED_DBG_CHECK(kb >= 0 && kb <= sh.P);
         if (i == sh.P) {
             int4 q = make_int4(s * sh.S, kb * sh.NP, s * sh.N, sh.N);
             reinterpret_cast<int4*>(segf)[s] = q;
         } else {
             const bool v = i < kb;
+            URED_DBG_CHECK(!v || (off[b * sh.P + i] >= 0 && counts[(size_t)b * sh.P + i] >= 0 &&
+                                  off[b * sh.P + i] + counts[(size_t)b * sh.P + i] <= sh.N));
             int4 q = make_int4(s * sh.S + i * sh.NP, v ? sh.NP : 0, off[b * sh.P + i] + h * (int)BN,
                                v ? (int)counts[(size_t)b * sh.P + i] : 0);
             reinterpret_cast<int4*>(segp)[s * sh.P + i] = q;
@@ -159,6 +162,7 @@ __global__ __launch_bounds__(LT) void cd_pair_reduce_kernel(CdShape sh, const fl
             float s0 = 0.f, s1 = 0.f;
             for (int p = t; p < sh.NP; p += LT) { s0 += daf[a0 + p]; s1 += dap[a0 + p]; }
             const int cnt = (int)counts[(size_t)b * sh.P + i];
+            URED_DBG_CHECK(kb <= sh.P && cnt >= 0 && off[b * sh.P + i] >= 0 && off[b * sh.P + i] + cnt <= sh.N);
             const long long b0 = (long long)off[b * sh.P + i] + (long long)h * sh.B * sh.N;
             float s2 = 0.f;
             for (int j = t; j < cnt; j += LT) s2 += dbp[b0 + j];
@@ -230,6 +234,7 @@ __global__ __launch_bounds__(LT) void cd_pair_grad_kernel(CdShape sh, const floa
         const int b = (int)(r / sh.N);
         gbf[t] = g4[2 * h] / ((float)sh.B * (float)sh.N);
         const int slot = gid[r], i = slot % sh.P;
+        URED_DBG_CHECK(slot >= 0);
         const int kb = (int)k[b];
         const long long cnt = counts[(size_t)b * sh.P + i];
         gbp[t] = (i < kb && cnt > 0) ? g4[2 * h + 1] / ((float)sh.B * (float)kb * (float)cnt) : 0.f;
@@ -294,6 +299,7 @@ __global__ __launch_bounds__(LT) void point_losses_fwd_kernel(PointLossArgs a) {
         const long long e0 = (long long)blk * PL_CHUNK, e1 = min((long long)a.B * a.N, e0 + PL_CHUNK);
         for (long long e = e0 + t; e < e1; e += LT) {
             const int b = (int)(e / a.N);
+            URED_DBG_CHECK((unsigned)a.knn[e] < (unsigned)a.S);
             const float* nn = a.out + 3 * ((long long)b * a.S + a.knn[e]);
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -440,6 +446,7 @@ __global__ __launch_bounds__(LT) void contrast_fwd_kernel(ContrastArgs a) {
     for (int j = t; j < a.n_all; j += LT) se += expf(lg[j] - m);
     se = block_sum(se, shf);
     const bool valid = a.src_labels[i] != -1;
+    URED_DBG_CHECK(!valid || (a.s_off + i >= 0 && a.s_off + i < a.n_all));   // the label's logit (LDS)
     if (t == 0) {
         const float l = m + logf(se);
         a.lse[i] = l;

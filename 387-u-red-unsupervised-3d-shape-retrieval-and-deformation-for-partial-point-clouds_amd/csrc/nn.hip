@@ -87,6 +87,9 @@ __global__ __launch_bounds__(NN_THREADS) void nn_fwd_kernel(NNFwdArgs args) {
     const int dir = (args.dirs == 2) ? 1 : (int)blockIdx.z;
     const float *Q, *R; int q_off, q_len, r_off, r_len; float* dist; int* idx;
     resolve_pair(args, dir, blockIdx.y, Q, R, q_off, q_len, r_off, r_len, dist, idx);
+    // a segment table entry must be non-negative and fit the launch's bounds (the grid covers
+    // max_q queries per segment; a longer segment would leave queries unwritten)
+    URED_DBG_CHECK(q_off >= 0 && r_off >= 0 && q_len >= 0 && r_len >= 0 && q_len <= (int)gridDim.x * QB);
     const int q0 = blockIdx.x * QB;
     if (q0 >= q_len) return;                 // uniform per block
     const int t = threadIdx.x, g = t / G, u = t % G;
@@ -210,6 +213,7 @@ __global__ __launch_bounds__(NN_THREADS) void nn_fwd_kernel(NNFwdArgs args) {
         if (qi >= q_len) continue;
         const int k0 = bchunk[i] * NN_CHUNK;
         const int kn = min(NN_CHUNK, r_len - k0);
+        URED_DBG_CHECK(k0 >= 0 && k0 < r_len);
         int bi = k0;
         for (int k = 0; k < kn; ++k) {
             float rx, ry, rz;
@@ -254,7 +258,9 @@ __global__ __launch_bounds__(NN_THREADS) void nn_bwd_kernel(NNBwdArgs args) {
     const float* pj = P + 3 * (size_t)(p_off + jc);
     const float px = pj[0], py = pj[1], pz = pj[2];
     float ax = 0.f, ay = 0.f, az = 0.f;
+    URED_DBG_CHECK(p_off >= 0 && o_off >= 0 && p_len >= 0 && o_len >= 0);
     if (o_len > 0 && gdP) {
+        URED_DBG_CHECK((unsigned)idxP[p_off + jc] < (unsigned)o_len);   // the NN index lies in the other side
         const float* r = O + 3 * (size_t)(o_off + idxP[p_off + jc]);
         const float g = gdP[p_off + jc] * 2.f;
         ax = g * (px - r[0]); ay = g * (py - r[1]); az = g * (pz - r[2]);
@@ -438,6 +444,7 @@ __global__ __launch_bounds__(64) void nn_fused_kernel(NNFusedArgs A) {
     const int qt = blockIdx.x % A.qtiles, rs = blockIdx.x / A.qtiles;
     int ao, al, bo, bl;
     seg_of(A, s, ao, al, bo, bl);
+    URED_DBG_CHECK(ao >= 0 && bo >= 0 && al >= 0 && bl >= 0 && ao + al <= A.a_total && bo + bl <= A.b_total);
     const int q0 = qt * 64 * QPT;
     const int r_begin = rs * A.rr;
     if (q0 >= al || r_begin >= bl) return;   // wave-uniform
@@ -551,6 +558,7 @@ __global__ __launch_bounds__(256) void nn_fused_finalize(NNFusedArgs A) {
         }
         const float v = __uint_as_float((unsigned)(key >> 32));
         const int k0 = (int)(unsigned)key * 16, kn = min(16, bl - k0);
+        URED_DBG_CHECK(ao + al <= A.a_total && k0 >= 0 && k0 < bl);
         const float* q = A.a + 3 * (size_t)(ao + j);
         int bi = k0;
         for (int k = 0; k < kn; ++k) {
@@ -570,6 +578,7 @@ __global__ __launch_bounds__(256) void nn_fused_finalize(NNFusedArgs A) {
         }
         const float v = __uint_as_float((unsigned)(key >> 32));
         const int k0 = (int)(unsigned)key * QPT, kn = min(QPT, al - k0);
+        URED_DBG_CHECK(bo + bl <= A.b_total && k0 >= 0 && k0 < al);
         const float* p = A.b + 3 * (size_t)(bo + j);
         int bi = k0;
         for (int k = 0; k < kn; ++k) {
@@ -657,8 +666,14 @@ __global__ __launch_bounds__(DCD_THREADS) void dcd_kernel(const float* __restric
     const float* D2 = d2 + (size_t)b * n2; const int* I2 = i2 + (size_t)b * n2;
     for (int k = t; k < n1 + n2; k += DCD_THREADS) cnt[k] = 0;
     __syncthreads();
-    for (int k = t; k < n1; k += DCD_THREADS) atomicAdd(&c1[I1[k]], 1);
-    for (int k = t; k < n2; k += DCD_THREADS) atomicAdd(&c2[I2[k]], 1);
+    for (int k = t; k < n1; k += DCD_THREADS) {
+        URED_DBG_CHECK((unsigned)I1[k] < (unsigned)n2);     // LDS counter index
+        atomicAdd(&c1[I1[k]], 1);
+    }
+    for (int k = t; k < n2; k += DCD_THREADS) {
+        URED_DBG_CHECK((unsigned)I2[k] < (unsigned)n1);
+        atomicAdd(&c2[I2[k]], 1);
+    }
     __syncthreads();
     auto wpow = [&](int c) {
         const float f = (float)c;
@@ -713,8 +728,10 @@ __global__ __launch_bounds__(256) void part_rows_bwd_kernel(const float* __restr
     const long long r = (long long)blockIdx.x * rows_per_block + lr;
     if (r >= rows) return;
     const long long b = r / N;
+    URED_DBG_CHECK(inv[r] >= 0 && inv[r] < N);
     const long long s = b * N + inv[r];
     const long long g = gid[s];
+    URED_DBG_CHECK(g >= 0);
     for (int c = threadIdx.x - lr * (per_row < 256 ? per_row : 256); c < per_row; c += 256) {
         if constexpr (V == 4) {
             float4 v = ds ? reinterpret_cast<const float4*>(ds + s * C)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -745,6 +762,7 @@ __global__ __launch_bounds__(256) void seg_aabb_kernel(const float* __restrict__
     __shared__ float red[6][4];
     const int g = blockIdx.x, t = threadIdx.x;
     const int r0 = off[g], r1 = off[g + 1];
+    URED_DBG_CHECK(r0 >= 0 && r1 >= r0);
     float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
     float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
     for (int r = r0 + t; r < r1; r += 256) {

@@ -142,6 +142,7 @@ __device__ __forceinline__ void node_combine(const UredNodeGemmDesc& d, const fl
         if (d.relu_out) v = fmaxf(v, 0.f);
         if (d.gate) v = d.gate[(long long)m * d.ldgate + n] > 0.f ? v : 0.f;
         if (d.R && n < d.R_ncols) v += d.R[(long long)m * d.ldR + n];
+        URED_DBG_CHECK(m < d.M && n < d.N && (!d.rowbias || m / d.rdiv >= 0));
         float* cp = d.C + (long long)m * d.ldc + n;
         if (d.accumulate) v += *cp;
         *cp = v;
@@ -301,6 +302,9 @@ struct Src4 {
     const float* base;   // operand base (uniform)
     unsigned vo;         // this lane's byte offset: row / column offset + its lane half's 16 k
     int sk4;             // k stride in bytes (4 for a k-contiguous operand)
+#if URED_DEBUG_BOUNDS
+    long long lim;       // bytes of the operand the job may read (node_v4_ok's extent)
+#endif
 };
 
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -310,6 +314,10 @@ template <bool KC>
 __device__ __forceinline__ void ld8(const Src4& s, int kb, float* out) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(s.base), (short)0,
                                                                         0x7FFFFFFF, 0x00020000);
+#if URED_DEBUG_BOUNDS
+    // the eight elements' last byte lies inside the extent node_v4_ok admitted for this operand
+    URED_DBG_CHECK(kb >= 0 && (long long)s.vo + (long long)(KC ? kb * 4 + 28 : (kb + 7) * (long long)s.sk4) + 4 <= s.lim);
+#endif
     if constexpr (KC) {
         const f4v x = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, s.vo, kb * 4, 0));
         const f4v y = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, s.vo, kb * 4 + 16, 0));
@@ -339,6 +347,9 @@ __device__ __forceinline__ void node_ring(const UredNodeGemmDesc& d, const Src4&
         sa.base = first ? a1.base : a2.base;
         sa.vo = first ? a1.vo : a2.vo;
         sa.sk4 = first ? a1.sk4 : a2.sk4;
+#if URED_DEBUG_BOUNDS
+        sa.lim = first ? a1.lim : a2.lim;
+#endif
         ld8<AKC>(sa, (first ? c0 : c0 - d.k1) + kh, a[slot]);
         ld8<BKC>(bs, c0 + kh, b[slot]);
     };
@@ -395,6 +406,17 @@ __global__ __launch_bounds__(NG_NT, URED_NODE_WG_PER_CU * NG_WAVES / 4) void nod
     const long long sbk = b2 ? d.sbk2 : d.sbk;
     bs.sk4 = (int)(sbk * 4);
     bs.vo = (unsigned)(((b2 ? (nc - d.n1) * d.sbn2 : nc * d.sbn) + 16LL * h * sbk) * 4);
+#if URED_DEBUG_BOUNDS
+    {   // the extents node_v4_ok bounds: the last element a source holds, + 1, in bytes
+        const int k1 = d.A2 ? d.k1 : d.K;
+        a1.lim = 4 * ((long long)(d.M - 1) * d.sam + (long long)((k1 < d.K ? k1 : d.K) - 1) * d.sak + 1);
+        if (d.A2) a2.lim = 4 * ((long long)(d.M - 1) * d.sam2 + (long long)(d.K - k1 - 1) * d.sak2 + 1);
+        else a2.lim = a1.lim;
+        if (!d.A || k1 <= 0) a1.lim = a2.lim;  // every chunk reads A2
+        bs.lim = b2 ? 4 * ((long long)(d.N - d.n1 - 1) * d.sbn2 + (long long)(d.K - 1) * d.sbk2 + 1)
+                    : 4 * ((long long)((d.B2 ? d.n1 : d.N) - 1) * d.sbn + (long long)(d.K - 1) * d.sbk + 1);
+    }
+#endif
 #if URED_NODE_TIMING
     const UredNodeGemmDesc& d0 = jobs.job[0].d;
     const bool nts_on = d0.M == URED_NTS_M && d0.N == URED_NTS_N && d0.K == URED_NTS_K && blockIdx.x < NTS_SLOTS;

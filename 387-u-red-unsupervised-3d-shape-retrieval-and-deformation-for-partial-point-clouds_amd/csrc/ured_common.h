@@ -31,6 +31,18 @@ inline int launch_status(const char* what) {
 
 }  // namespace ured
 
+// Debug build (-DURED_DEBUG_BOUNDS=1): device-side bounds checks of the indices a kernel derives
+// from its arguments or reads from device tables (segment tables, NN indices, labels), and of the
+// raw buffer offsets of the MFMA kernels; a violation traps (the launch fails with a fault that
+// names the kernel). Compiled out (no code) in the default build.
+#ifndef URED_DEBUG_BOUNDS
+#define URED_DEBUG_BOUNDS 0
+#endif
+#define URED_DBG_CHECK(cond)                                     \
+    do {                                                         \
+        if (URED_DEBUG_BOUNDS && !(cond)) __builtin_trap();      \
+    } while (0)
+
 #define URED_REQUIRE(cond, ...)                                  \
     do {                                                         \
         if (!(cond)) return ured::set_error(URED_EINVAL, __VA_ARGS__); \

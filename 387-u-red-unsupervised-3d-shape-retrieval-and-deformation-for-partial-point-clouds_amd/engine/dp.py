@@ -20,7 +20,12 @@ gradient buffer, in buckets of ~bucket_mb MB that are issued DURING backward:
     a full bucket's gradients are copied into their flat views (one multi-tensor copy) and its
     all_reduce is issued asynchronously (RCCL runs it on its own stream after the copy, while
     backward continues on the compute stream). Buckets are issued strictly in index order, as
-    DDP does, so every rank issues the same collectives in the same order;
+    DDP does, so every rank issues the same collectives in the same order. Buckets are cut from
+    the end of that order: the last one (whose all-reduce is left after the backward) is small
+    (cfg "dp_last_bucket_mb", 4 MB), the others ~bucket_mb. Every collective goes through
+    ured_hip/collective.run(), so a HIP-graph capture of the step (engine/graph.py) either
+    captures them (RCCL, inline) or splits the captured backward at each bucket and issues the
+    bucket's all-reduce between the segments of every replay, overlapping the later segments;
   * after backward: buckets that did not fill (a parameter without a gradient this step) are
     completed with zeros for the missing parameters and reduced; parameters with a gradient
     outside every bucket (one that just became active) are reduced as extra ranges; then the
@@ -34,6 +39,7 @@ import torch
 import torch.distributed as dist
 
 from engine.train import CLIPPED, TrainStep
+from ured_hip import collective
 
 
 def make_buckets(params, bucket_elems):
@@ -103,8 +109,10 @@ class FlatGradReducer:
     """Bucketed all-reduce of FlatAdam's flat gradient, issued from backward's gradient hooks
     (see the module docstring). Usage per step: begin() before backward, finish() after it."""
 
-    def __init__(self, optimizer, params, world, bucket_elems, overlap=True):
+    def __init__(self, optimizer, params, world, bucket_elems, overlap=True, last_elems=None):
         self.opt, self.world, self.bucket_elems, self.overlap = optimizer, world, bucket_elems, overlap
+        self.last_elems = bucket_elems if last_elems is None else max(1, int(last_elems))
+        self.issued = []                    # bucket indices in all-reduce issue order (tests clear / read it)
         self._arrival = []                  # first step: gradient arrival order
         self._fb = None                     # buckets over the flat gradient
         self._fb_key = None
@@ -126,12 +134,17 @@ class FlatGradReducer:
             return                        # not in a bucket: handled after backward
         b.pending -= 1
         if b.pending == 0 and b.idx == self._next:
-            fb = self._fb
+            fb, ready = self._fb, []
             while self._next < len(fb) and fb[self._next].pending == 0:
-                self._launch(fb[self._next])
+                self._prepare(fb[self._next])
+                ready.append(fb[self._next])
                 self._next += 1
+            collective.run(self._issue_fn(ready))     # one host step (one graph split) per hook
 
-    def _launch(self, b, fill_missing=False):
+    def _prepare(self, b, fill_missing=False):
+        """The GPU side of a bucket before its all-reduce: gradients that are not their flat views
+        (torch-produced) copied in, missing ones zeroed (after backward only). Captured into the
+        current graph segment when a graph capture is running."""
         dst, src = [], []
         for p, v in zip(b.params, b.views):
             g = p.grad
@@ -144,25 +157,62 @@ class FlatGradReducer:
                 src.append(g)
         if dst:
             torch._foreach_copy_(dst, src)
-        b.work = dist.all_reduce(self.opt.flat_grad[b.beg:b.end], op=dist.ReduceOp.SUM, async_op=True)
         b.launched = True
 
+    def _issue_fn(self, bs, wait=()):
+        """The host side: all_reduce of each bucket's flat slice (async) issued in bucket order,
+        then the waits of `wait`. Goes through collective.run(): eagerly it runs at once; while a
+        segmented capture records the step (engine/graph.py) it closes the graph segment and runs
+        between segments at every replay — after the kernels that wrote the bucket, before the
+        rest of the backward, so the reduction overlaps it."""
+        flat = self.opt.flat_grad
+        views = [flat[b.beg:b.end] for b in bs]
+
+        def fn():
+            for b, v in zip(bs, views):
+                b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, async_op=True)
+                self.issued.append(b.idx)
+            for b in wait:
+                b.work.wait()
+        return fn
+
+    def _reduce_ranges(self, ranges):
+        """Average [beg, end) ranges of the flat gradient outside the buckets: <= bucket_elems views
+        all-reduced (issued, then waited, through collective.run), then scaled by 1/world."""
+        flat = self.opt.flat_grad
+        views = [flat[o:min(e, o + self.bucket_elems)] for b, e in ranges for o in range(b, e, self.bucket_elems)]
+
+        def fn():
+            works = [dist.all_reduce(v, op=dist.ReduceOp.SUM, async_op=True) for v in views]
+            for w in works:
+                w.wait()
+        collective.run(fn)
+        for b, e in ranges:
+            flat[b:e].mul_(1.0 / self.world)
+
     def _build(self):
+        """Buckets over the flat gradient in backward's production order, cut from the END: the
+        last bucket (the last gradients backward produces, whose all-reduce is the one left
+        exposed after the backward) holds ~last_elems elements, the others ~bucket_elems. A bucket
+        is a contiguous range (parameters without a gradient this step split it)."""
         from ured_hip.optim import _aligned
         opt = self.opt
         slot = sorted((opt._off[i], i) for i, a in enumerate(opt._active) if a)
-        fb, cur, beg, end, n = [], [], 0, 0, 0
-        for o, i in slot:
-            if cur and (o != end or n >= self.bucket_elems):
-                fb.append(_Bucket(len(fb), beg, end, [opt.params_all[j] for j in cur], [opt._gviews[j] for j in cur]))
-                cur, n = [], 0
-            if not cur:
-                beg = o
+        groups, cur, beg, n, limit = [], [], 0, 0, self.last_elems
+        for o, i in reversed(slot):
+            if cur and (o + _aligned(opt.params_all[i].numel()) != beg or n >= limit):
+                groups.append(cur)
+                cur, n, limit = [], 0, self.bucket_elems
             cur.append(i)
-            end = o + _aligned(opt.params_all[i].numel())
+            beg = o
             n += opt.params_all[i].numel()
         if cur:
-            fb.append(_Bucket(len(fb), beg, end, [opt.params_all[j] for j in cur], [opt._gviews[j] for j in cur]))
+            groups.append(cur)
+        fb = []
+        for g in reversed(groups):
+            g = g[::-1]
+            fb.append(_Bucket(len(fb), opt._off[g[0]], opt._off[g[-1]] + _aligned(opt.params_all[g[-1]].numel()),
+                              [opt.params_all[j] for j in g], [opt._gviews[j] for j in g]))
         self._fb, self._fb_key = fb, opt._active
         self._bucket_of = {id(p): b for b in fb for p in b.params}
 
@@ -190,14 +240,18 @@ class FlatGradReducer:
 
     def finish(self):
         """After backward: complete the reduction; the flat gradient holds the rank average and
-        p.grad of every active parameter is its flat view."""
+        p.grad of every active parameter is its flat view. Every collective goes through
+        collective.run(), every tensor op stays on the stream: called inside a graph capture
+        (engine/graph.py) the whole reduction is part of the captured step, its collectives either
+        captured (RCCL, inline) or issued between the graph segments at every replay."""
         self._armed = False
         armed, self._step_armed = self._step_armed, False
         opt = self.opt
         if opt.flat_param is None and self._arrival:
             opt.layout_order = list(self._arrival)        # first step: backward's order
         active = opt.prepare()
-        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        if capturing:
             # a captured finish() must not sync (the layout check reads its all-reduced hash on
             # the host) nor rebuild the buckets (their ranges are baked into the graph): the eager
             # step of the same key, which always runs before its capture, has done both
@@ -210,22 +264,25 @@ class FlatGradReducer:
             # all_reduce, only when the set changes)
             self._check_layout()
         if not armed or not any(b.launched for b in self._fb):
-            # first step (overlap off, a captured step, or no bucket filled): all after backward
+            # first step (overlap off, or no bucket filled during backward): all after backward
             opt.gather_grads()
-            allreduce_flat(opt.flat_grad, self.world, self.bucket_elems, opt.active_ranges())
+            self._reduce_ranges(opt.active_ranges())
+            opt.mark_gathered()
             if self.overlap and self._fb_key != active:
                 self._build()
             return
-        for b in self._fb[self._next:]:                   # buckets that did not fill, in order
-            self._launch(b, fill_missing=True)
+        rest = self._fb[self._next:]                      # buckets that did not fill, in order
+        for b in rest:
+            self._prepare(b, fill_missing=True)
         extra = [i for i, a in enumerate(active) if a and id(opt.params_all[i]) not in self._bucket_of]
+        if extra and capturing:
+            raise RuntimeError("data-parallel: a parameter outside every bucket inside a graph capture")
         for i in extra:                                   # parameters that just became active
             opt._gviews[i].copy_(opt.params_all[i].grad)
-        for b in self._fb:
-            b.work.wait()
+        # the remaining buckets' all-reduces and the waits of every bucket, as one host step
+        collective.run(self._issue_fn(rest, wait=self._fb))
         if extra:
-            allreduce_flat(opt.flat_grad, self.world, self.bucket_elems,
-                           [(opt._off[i], opt._off[i] + opt.params_all[i].numel()) for i in extra])
+            self._reduce_ranges([(opt._off[i], opt._off[i] + opt.params_all[i].numel()) for i in extra])
         for b in self._fb:
             opt.flat_grad[b.beg:b.end].mul_(1.0 / self.world)
         opt.mark_gathered()
@@ -238,7 +295,7 @@ class DataParallelStep(TrainStep):
     contrastive all_gather) through the process group even at world size 1 — the test hook that
     exercises the RCCL code paths, eager and captured, on a one-GPU box."""
 
-    def __init__(self, cfg, db, device, bucket_mb=25.0, overlap=None):
+    def __init__(self, cfg, db, device, bucket_mb=25.0, overlap=None, last_bucket_mb=None):
         super().__init__(cfg, db, device)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.collect = self.world > 1 or (bool(cfg.get("dp_force_collectives", False)) and dist.is_initialized())
@@ -252,7 +309,11 @@ class DataParallelStep(TrainStep):
         self.bucket_elems = int(bucket_mb * 1e6 / 4)
         self._buckets = None                # torch-Adam path: (active key, buckets)
         overlap = self.collect if overlap is None else bool(overlap)
-        self.reducer = (FlatGradReducer(self.optimizer, params, self.world, self.bucket_elems, overlap)
+        # the last bucket is the one whose all-reduce follows the backward: kept small (cfg
+        # "dp_last_bucket_mb", default 4 MB; the others ~bucket_mb)
+        last_mb = cfg.get("dp_last_bucket_mb", 4.0) if last_bucket_mb is None else last_bucket_mb
+        self.reducer = (FlatGradReducer(self.optimizer, params, self.world, self.bucket_elems, overlap,
+                                        last_elems=int(last_mb * 1e6 / 4))
                         if self.collect and hasattr(self.optimizer, "prepare") else None)
 
     def broadcast_state(self, src=0):

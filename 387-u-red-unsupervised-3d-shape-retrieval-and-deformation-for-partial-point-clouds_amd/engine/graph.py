@@ -6,8 +6,8 @@ autograd engine; at ~20 ms of GPU work per step that host cost is the same order
 time. The step has no host sync (segment tables, part pooling and the unique-source tables
 are built on the device or from host labels before the step), so it is captured and replayed:
 
-  graph "fwd_bwd"[key] : grads.zero_() + forward + backward
-  eager                : reduce_gradients()      (RCCL bucketed all-reduce when world > 1)
+  graph "fwd_bwd"[key] : grads.zero_() + forward + backward (+ the data-parallel gradient
+                         reduction when world > 1, see below)
   graph "update"       : clip_grad_norm_ x6 + Adam (capturable); FlatAdam reads the learning
                          rate from a device scalar, torch's optimizers get the update graph
                          re-captured when a scheduler changes the lr
@@ -30,18 +30,27 @@ the same state and batch.
 
 Data parallel (world > 1): the forward contains collectives — the contrastive loss's all_gather
 of the source codes and, with SyncBN, every BN layer's statistics exchange — and the backward
-the bucketed gradient all-reduce.
-  * RCCL ("nccl"): the collectives are captured in the graph (SegmentedCapture(inline=True)): the
-    hooks of engine/dp.py issue each gradient bucket's all-reduce on RCCL's stream as soon as
-    the bucket's last gradient is written, so in the replayed graph the reduction overlaps the
-    rest of the backward, and reduce_gradients() (waits, scaling) is captured after it.
-  * gloo (the CPU / one-GPU rehearsal backend; its collectives cannot be captured): the fwd_bwd
-    region is captured as a chain of graphs split at each collective (ured_hip/collective.py),
-    a replay runs segment, collective, segment, ... with the collectives issued eagerly on the
-    segments' static buffers, and the gradient all-reduce follows the replay. The gradients of
-    the parameters that torch (not a HIP layer) produces are copied into their flat-gradient
-    views INSIDE the last segment, so that all-reduce reads every gradient of this step and the
-    update graph contains no copy that could overwrite the averaged values.
+the bucketed gradient all-reduce (engine/dp.py FlatGradReducer: each bucket of the flat gradient
+is all-reduced as soon as backward has written its last gradient). The whole reduction —
+bucket all-reduces, their waits and the 1/world scaling — is part of the captured step, in one
+of two forms:
+  * segmented (the default at world > 1, RCCL or gloo; ured_hip/collective.py): the capture is a
+    chain of graphs split at each collective. A replay runs segment 0, collective 0, segment 1, ...
+    with the collectives issued eagerly on the segments' static buffers: a bucket's all_reduce is
+    issued (async, on the process group's stream) right after the segment that wrote the bucket's
+    last gradient and runs while the next segments — the rest of the backward — replay; the waits
+    come after the last backward segment and the scaling is the last segment's tail. So only the
+    last bucket's all-reduce (the last gradients backward produces; engine/dp.py keeps that
+    bucket small, cfg "dp_last_bucket_mb") follows the backward. Every eager step issues the same
+    bucket sequence from the same hooks, so ranks that capture at different steps still issue
+    identical collective sequences. Tested at world 2 with gloo on one GPU
+    (tests/test_graph_dp_gpu.py: replay == eager bitwise, bucket issue order); not yet run with
+    RCCL at world > 1 (no multi-GPU box has run it).
+  * inline (RCCL at world size 1 — tests/test_nccl_gpu.py — or cfg["graph_inline_collectives"]):
+    the collectives are captured in the graph itself (SegmentedCapture(inline=True)), one graph,
+    the bucket all-reduces on RCCL's stream inside it.
+With torch's optimizers (no flat gradient) the capture holds no gradient reduction: it runs
+eagerly after the replay (engine/dp.py allreduce_gradients).
 """
 from collections import OrderedDict
 
@@ -119,13 +128,19 @@ class GraphedStep:
         steps (keys follow each rank's batches), so the inline form rests on every rank's eager
         collective sequence matching another rank's replayed one; until a multi-GPU RCCL run has
         checked averaged gradients and parameters against eager steps, world > 1 takes the
-        segmented capture (collectives eagerly between graph segments, the gradient all-reduce
-        after the replay) unless cfg["graph_inline_collectives"] asks for the inline form."""
+        segmented capture (collectives eagerly between graph segments, each gradient bucket's
+        all-reduce issued between the backward segments) unless cfg["graph_inline_collectives"]
+        asks for the inline form."""
         import torch.distributed as dist
         if not (getattr(self.inner, "collect", False) and dist.is_initialized() and dist.get_backend() == "nccl"):
             return False
         flag = self.inner.cfg.get("graph_inline_collectives")     # None: by world size; True / False: forced
         return dist.get_world_size() == 1 if flag is None else bool(flag)
+
+    def _reduce_in_capture(self):
+        """The gradient reduction is captured with the step (FlatGradReducer: every collective
+        through collective.run, every tensor op on the stream); otherwise it runs after a replay."""
+        return getattr(self.inner, "reducer", None) is not None
 
     def _flat(self):
         """FlatAdam: the HIP layers write the gradients into its persistent flat buffer."""
@@ -145,10 +160,10 @@ class GraphedStep:
             return _detached(T)
         self._fresh_grads()
         loss, T = self.inner.forward(batch, epoch)
-        if self._inline():
-            # the same bucketed all-reduces as a replay of the captured graph issues; with gloo the
-            # replay reduces after the backward, and so does this step (ranks can miss a graph at
-            # different steps: their collective sequences must still match)
+        if self._inline() or self._reduce_in_capture():
+            # the same bucketed all-reduces, from the same hooks, as a replay of the captured step
+            # issues (ranks can miss a graph at different steps: their collective sequences must
+            # still match)
             self.inner.begin_backward()
         loss.backward()
         del loss
@@ -165,6 +180,7 @@ class GraphedStep:
         if flat:
             self.inner.optimizer.zero_grad(set_to_none=True)
         inline = self._inline()
+        reduced = inline or self._reduce_in_capture()
         cap = SegmentedCapture(inline=inline)
         stream = torch.cuda.Stream()
         stream.wait_stream(torch.cuda.current_stream())
@@ -174,11 +190,11 @@ class GraphedStep:
                 if not flat:
                     torch._foreach_zero_(self.grads)
                 loss, T = self.inner.forward(static, epoch)
-                if inline:
-                    self.inner.begin_backward()      # bucket all-reduces from the hooks, captured
+                if reduced:
+                    self.inner.begin_backward()      # bucket all-reduces from the hooks
                 loss.backward()
-                if inline:
-                    self.inner.reduce_gradients()    # completes the captured reduction (flat views)
+                if reduced:
+                    self.inner.reduce_gradients()    # remaining buckets, waits, 1/world (flat views)
                 elif flat:
                     # torch-produced gradients into their flat views, inside the captured region
                     self.inner.optimizer.gather_grads()
@@ -196,7 +212,7 @@ class GraphedStep:
         del loss
         if self.g_update is None:
             self._capture_update()
-        self.graphs[key] = (static, cap, T, inline)
+        self.graphs[key] = (static, cap, T, reduced)
         while len(self.graphs) > self.max_graphs:
             self.graphs.popitem(last=False)
 
@@ -215,6 +231,9 @@ class GraphedStep:
         self.update_captures = getattr(self, "update_captures", 0) + 1
 
     def step(self, batch, epoch=0):
+        if not self.inner.cfg.get("unique_sources", True) and "src_unique" in batch:
+            # every slot encoded: the distinct-part tables are not read (and not part of the key)
+            batch = {n: v for n, v in batch.items() if n != "src_unique"}
         k = self.key(batch, epoch)
         if self.grads is not None and getattr(self, "_gate", None) is not None and k[1] != self._gate:
             self.graphs.clear()          # another parameter set: re-learn the gradients eagerly
@@ -234,10 +253,10 @@ class GraphedStep:
             self._capture(k, batch, epoch)
             return T
         self.graphs.move_to_end(k)
-        static, cap, T, inline = ent
+        static, cap, T, reduced = ent
         refresh_static(static, batch)        # one ured_copy_batch launch for the input tensors
         cap.replay()                         # segments, and the collectives between them
-        if not inline:
+        if not reduced:
             self.inner.reduce_gradients()
         sync = getattr(self.inner.optimizer, "sync_lr", None)
         if sync is not None:                 # FlatAdam reads lr from a device scalar

@@ -109,7 +109,7 @@ def _reducer_worker(rank, world, port, q):
         params = [p for m in mods for p in m.parameters()]
         opt = FlatAdam(params, [list(mods[0].parameters()) + list(mods[1].parameters()),
                                 list(mods[2].parameters()) + list(mods[3].parameters()) + list(mods[4].parameters())])
-        red = FlatGradReducer(opt, params, world, bucket_elems=40, overlap=True)
+        red = FlatGradReducer(opt, params, world, bucket_elems=40, overlap=True, last_elems=12)
 
         def fwd(ms, x, use3):
             h = ms[2](torch.relu(ms[1](torch.relu(ms[0](x)))))
@@ -125,6 +125,8 @@ def _reducer_worker(rank, world, port, q):
             fwd(ref, x, use3).backward()
             local = [p.grad.clone() if p.grad is not None else None for r in ref for p in r.parameters()]
             opt.zero_grad(set_to_none=True)
+            nb_before = red.num_buckets
+            red.issued.clear()
             red.begin()
             fwd(mods, x, use3).backward()
             res["overlapped"].append(red._fb is not None and any(b.launched for b in red._fb))
@@ -139,7 +141,14 @@ def _reducer_worker(rank, world, port, q):
                 ok &= bool(torch.allclose(p.grad, torch.stack(allg).mean(0), atol=1e-6))
                 ok &= p.grad.data_ptr() >= opt.flat_grad.data_ptr()      # a view of the flat buffer
             res["ok"].append(ok)
-            res["buckets"].append(red.num_buckets)
+            res["buckets"].append(sum(len(b.params) for b in red._fb))
+            # buckets are all-reduced strictly in index order, every one of them once
+            res["order_ok"] = res.get("order_ok", True) and red.issued == list(range(nb_before))
+            res.setdefault("nbuckets", []).append(red.num_buckets)
+            # the last bucket (the one left after backward) is cut at ~last_elems
+            fb = red._fb
+            res["last_small"] = res.get("last_small", True) and (
+                len(fb) < 2 or sum(p.numel() for p in fb[-1].params[1:]) < red.last_elems)
             with torch.no_grad():                          # the same update on both copies
                 for p, r in zip(params, [p for r in ref for p in r.parameters()]):
                     if p.grad is not None:
@@ -167,4 +176,6 @@ def test_flat_grad_reducer_gloo_world2():
     for r in res:
         assert r["ok"] == [True] * 4, r
         assert r["overlapped"] == [False, True, True, True], r
-        assert r["buckets"][0] > 1 and r["buckets"][3] > r["buckets"][1], r
+        # bucketed parameters: the one joining at step 3 is bucketed from then on
+        assert r["nbuckets"][0] > 1 and r["buckets"][3] > r["buckets"][1], r
+        assert r["order_ok"] and r["last_small"], r

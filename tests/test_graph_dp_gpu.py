@@ -1,7 +1,9 @@
 """Graph replay of the DATA-PARALLEL step (engine/graph.py with world > 1): the captured step is a
 chain of graphs split at its collectives (the contrastive loss's all_gather; with SyncBN every
-BN statistics exchange), replayed with the collectives issued eagerly between the segments
-(ured_hip/collective.py), then the eager gradient all-reduce and the update graph.
+BN statistics exchange) and at the gradient buckets the backward's hooks all-reduce, replayed
+with the collectives issued eagerly between the segments (ured_hip/collective.py: each bucket's
+all-reduce right after the segment that wrote it, overlapping the rest of the backward; the
+waits and the 1/world scaling at the end of the captured region), then the update graph.
 
 gloo world 2, both ranks on the one GPU of the test box, each rank its own batches. Per rank, an
 eager DataParallelStep and a GraphedStep over another DataParallelStep (same initial weights)
@@ -55,16 +57,23 @@ def _worker(rank, world, port, sync_bn, q):
         # one padded distinct-part count for all batches: one graph, three replays
         batches = [batch_to_device(synthetic.make_batch(2, 128, 24, parts=[3, 2], seed=100 * rank + i), dev, 24,
                                    bucket=16) for i in range(4)]
+        # small buckets, so that the captured backward is split at several bucket all-reduces
         torch.manual_seed(5)
-        a = DataParallelStep(cfg, db, dev)
+        a = DataParallelStep(cfg, db, dev, bucket_mb=0.5, last_bucket_mb=0.1)
         torch.manual_seed(5)
-        b = DataParallelStep(cfg, db, dev)
+        b = DataParallelStep(cfg, db, dev, bucket_mb=0.5, last_bucket_mb=0.1)
         g = GraphedStep(a)
         same_loss = True
+        orders, eager_orders = [], []
         for i, bt in enumerate(batches):
+            a.reducer.issued.clear()
+            b.reducer.issued.clear()
             la = g.step(bt)["all_loss"].clone()
             lb = b.step(bt)["all_loss"]
+            orders.append(list(a.reducer.issued))
+            eager_orders.append(list(b.reducer.issued))
             same_loss &= bool(torch.equal(la, lb))
+        res["orders"], res["eager_orders"], res["nbuckets"] = orders, eager_orders, a.reducer.num_buckets
         ent = next(iter(g.graphs.values()))
         res["segments"], res["collectives"] = len(ent[1].graphs), len(ent[1].collectives)
         res["ngraphs"] = len(g.graphs)
@@ -116,6 +125,16 @@ def test_graph_dp_replay_equals_eager(dev, sync_bn):
               f"collectives, {r['n_tensors']} tensors compared")
         assert r["ngraphs"] == 1
         assert r["collectives"] >= 1 and r["segments"] == r["collectives"] + 1
+        # the gradient buckets are all-reduced from the replayed step, between its backward
+        # segments, strictly in bucket order (step 0 runs eagerly before any bucket exists, then
+        # is captured: its collectives are recorded, not issued); the eager steps issue the same
+        nb = r["nbuckets"]
+        assert nb >= 3, r
+        assert r["orders"][0] == [] and all(o == list(range(nb)) for o in r["orders"][1:]), r["orders"]
+        assert r["eager_orders"][0] == [] and all(o == list(range(nb)) for o in r["eager_orders"][1:])
+        # at least one split per bucket hook beyond the forward's all_gather (several buckets can
+        # fill at one hook and share a split)
+        assert r["collectives"] >= 3, r
         if sync_bn:
             assert r["collectives"] > 20           # every BN layer's exchange, forward and backward
         assert r["grads_are_views"]
