@@ -931,48 +931,6 @@ __device__ __forceinline__ float pro_v(float x, float s, float t) {
     return x;
 }
 
-// Epilogue token (round 6). The two blocks a CU holds run the same program, so they fall into
-// lockstep: both reach their epilogue (no MFMA work: operand loads, VALU, stores, reductions) at the
-// same time and leave the CU's matrix pipes idle for its whole length (GEMM design). A
-// per-CU token in global memory lets one block at a time into its epilogue: when both arrive
-// together, the second waits while the first's epilogue runs beside nothing, and from then on the
-// pair runs out of phase — each epilogue beside the other block's K-loop. The token is a
-// scheduling hint only: a block that cannot take it within a bounded spin proceeds without it
-// (no deadlock whatever the residency, a stale token from an aborted launch only costs the
-// spin), and the arithmetic is unchanged (results bitwise identical with the token on or off).
-// Slots: one per (XCC, SE, SH, CU) of HW_ID; two CUs sharing a slot only share a hint.
-#ifndef URED_EPI_TOKEN
-#define URED_EPI_TOKEN 1
-#endif
-#ifndef URED_EPI_TOKEN_MIN_TILES
-#define URED_EPI_TOKEN_MIN_TILES 1024    // launches of >= 2 rounds of tiles at two blocks per CU
-#endif
-#ifndef URED_EPI_TOKEN_SPIN
-#define URED_EPI_TOKEN_SPIN 4096         // polls of ~0.1-1 us before proceeding without the token
-#endif
-constexpr int EPI_TOKEN_SLOTS = 8 * 256;
-__device__ unsigned ured_epi_token[EPI_TOKEN_SLOTS];
-
-__device__ __forceinline__ unsigned* epi_token_slot() {
-    const unsigned hw = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-    const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-    const unsigned cu = (hw >> 8) & 0xF, sh = (hw >> 12) & 1, se = (hw >> 13) & 7;
-    return &ured_epi_token[((xcc & 7) << 8) | (se << 5) | (sh << 4) | cu];
-}
-
-// one lane: compare-and-swap 0 -> 1 on the slot, polling with a sleep; true if taken
-__device__ __forceinline__ bool epi_token_take(unsigned* p) {
-#pragma unroll 1
-    for (int i = 0; i < URED_EPI_TOKEN_SPIN; ++i) {
-        unsigned expected = 0u;
-        if (__hip_atomic_compare_exchange_strong(p, &expected, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-            return true;
-        __builtin_amdgcn_s_sleep(4);
-    }
-    return false;
-}
-
 // TM / TN: 32-row / 32-column MFMA tiles per wave (2 x 2 waves per block), so the block tile is
 // (64 TM) x (64 TN): 128 x 128 for the wide layers; TN = 1 (128 x 64) for outputs of <= 64
 // columns and TM = 1 (64 x ...) for split-K / store GEMMs of <= 64 output rows — the 32- and
@@ -1197,25 +1155,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(const UredGemmDesc d) {
 #if URED_GEMM_TIMING
     ts_[2] = __builtin_amdgcn_s_memrealtime();
 #endif
-#if URED_EPI_TOKEN
-    // one block of the CU's pair in its epilogue at a time (see epi_token_slot); only in launches
-    // long enough for the pair to settle out of phase
-    const bool token = ntiles * (int)gridDim.z >= URED_EPI_TOKEN_MIN_TILES;
-    __shared__ int tok_held;
-    unsigned* tok = nullptr;
-    if (token) {
-        tok = epi_token_slot();
-        if (t == 0) tok_held = epi_token_take(tok) ? 1 : 0;
-        lds_barrier();                       // the other waves wait for wave 0's take
-    }
-#endif
     epilogue<EPI, true, TM, TN>(d, acc, m0, n0, red_f, red_i);
-#if URED_EPI_TOKEN
-    if (token) {
-        lds_barrier();                       // every wave has issued its epilogue
-        if (t == 0 && tok_held) __hip_atomic_store(tok, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#endif
 #if URED_GEMM_TIMING
     if (ts_on) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

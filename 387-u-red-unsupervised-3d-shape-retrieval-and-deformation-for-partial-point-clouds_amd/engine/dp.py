@@ -113,6 +113,7 @@ class FlatGradReducer:
         self.opt, self.world, self.bucket_elems, self.overlap = optimizer, world, bucket_elems, overlap
         self.last_elems = bucket_elems if last_elems is None else max(1, int(last_elems))
         self.issued = []                    # bucket indices in all-reduce issue order (tests clear / read it)
+        self.deferred = []                  # captured hooks that ran off the capture stream (diagnostics)
         self._arrival = []                  # first step: gradient arrival order
         self._fb = None                     # buckets over the flat gradient
         self._fb_key = None
@@ -133,6 +134,14 @@ class FlatGradReducer:
         if b is None:
             return                        # not in a bucket: handled after backward
         b.pending -= 1
+        cs = collective.capture_stream()
+        if cs is not None and torch.cuda.current_stream() != cs:
+            # a captured step whose hook runs on another stream than the capture's (the autograd
+            # engine runs a parameter's gradient accumulation on the stream its accumulator node was
+            # created on): a graph split or a copy from here would not land in the captured
+            # sequence. The bucket is left to finish(), on the capture stream, in the same order.
+            self.deferred.append((b.idx, int(torch.cuda.current_stream().stream_id), int(cs.stream_id)))
+            return
         if b.pending == 0 and b.idx == self._next:
             fb, ready = self._fb, []
             while self._next < len(fb) and fb[self._next].pending == 0:

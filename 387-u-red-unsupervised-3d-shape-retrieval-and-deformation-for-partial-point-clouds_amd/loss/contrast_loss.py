@@ -40,7 +40,10 @@ def all_gather_batch(tensors, differentiable=False, force=False):
     out = []
     for t in tensors:
         bufs = [torch.empty_like(t) for _ in range(world)]
-        tc = t.contiguous()
+        # detached: the closure lives as long as a captured step that replays it, and a tensor
+        # with autograd history would keep that step's autograd graph (and the AccumulateGrad
+        # nodes, bound to the capture's stream) alive into later captures (engine/dp.py)
+        tc = t.detach().contiguous()
         # eager, or between two segments of a captured step (ured_hip/collective.py)
         collective.run(lambda bufs=bufs, tc=tc: dist.all_gather(bufs, tc))
         if differentiable:

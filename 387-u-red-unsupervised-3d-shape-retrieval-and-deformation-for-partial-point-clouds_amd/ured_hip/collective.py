@@ -14,6 +14,12 @@ rest of the backward on RCCL's stream, engine/graph.py).
 """
 
 _split = None
+_active = None          # the SegmentedCapture being recorded (segmented or inline), else None
+
+
+def capture_stream():
+    """The stream the running segmented capture records on (None when nothing is captured)."""
+    return None if _active is None else _active.stream
 
 
 def run(fn):
@@ -49,7 +55,12 @@ class SegmentedCapture:
         self._g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
 
     def _close(self):
-        self._g.capture_end()
+        # two collectives with no kernel between them (e.g. the last gradient bucket's all-reduce
+        # and the waits after the backward) leave an empty segment: valid, replays as a no-op
+        import warnings
+        with warnings.catch_warnings():
+            warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
+            self._g.capture_end()
         self.graphs.append(self._g)
         self._g = None
 
@@ -59,22 +70,26 @@ class SegmentedCapture:
         self._open()
 
     def begin(self):
-        global _split
-        if _split is not None:
+        global _split, _active
+        if _split is not None or _active is not None:
             raise RuntimeError("nested segmented capture")
+        self.stream = self._torch.cuda.current_stream()
         self._open()
+        _active = self
         if not self.inline:
             _split = self._split_at
 
     def end(self):
-        global _split
+        global _split, _active
         _split = None
+        _active = None
         self._close()
 
     def abort(self):
         """After an exception inside the captured region: leave capture mode."""
-        global _split
+        global _split, _active
         _split = None
+        _active = None
         if self._g is not None:
             try:
                 self._g.capture_end()

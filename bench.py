@@ -848,6 +848,12 @@ def main():
         extra["loader_iters_s"] = loader["iters_s"]
         extra["loader"] = loader
     extra["unique_sources"] = bool(cfg["unique_sources"])
+    red = getattr(eager, "reducer", None)
+    if world > 1 and red is not None:
+        # gradient buckets all-reduced between the captured backward's segments; hooks that ran off
+        # the capture stream leave their bucket to the end of the backward (engine/dp.py)
+        extra["dp_overlap"] = {"buckets": red.num_buckets, "deferred_hooks": len(red.deferred),
+                               "deferred_sample": red.deferred[:4]}
     if not args.no_extras:
         ch = chamfer_rate(dev)
         extra["chamfer_gpair_s"] = ch["gpair_dist_s"]

@@ -119,7 +119,15 @@ def _worker(rank, world, port, bs, npts, q):
 # regime that exists only in this one-GPU rehearsal (production runs one rank per GPU). Two per
 # rank keeps the 8-rank rehearsal at the 4-rank one's queue count ("The multi-process
 # fault").
-RANK_HW_QUEUES = "2"
+# What this cap means for the evidence: the HSA_STATUS_ERROR_ILLEGAL_INSTRUCTION aborts of rounds
+# 3 and 4 happened in the UNCAPPED 8-rank run (nine processes x 4 queues). With the cap, the
+# 8-rank test no longer runs in that regime, so its green runs do not show that the round-5
+# change (the compiler's LDS-DMA builtin issued ahead of the MFMAs) removed the cause; they show
+# that the data-parallel step is correct at eight ranks. The memory-safety side is checked
+# separately: the single-process suite on the bounds-checked build (tools/debug_bounds_suite.sh).
+# URED_TEST_RANK_HW_QUEUES overrides the cap ("default": no cap, the r3 / r4 regime) for a
+# deliberate diagnostic run; the suite's default keeps it.
+RANK_HW_QUEUES = os.environ.get("URED_TEST_RANK_HW_QUEUES", "2")
 
 
 def _run(world, bs, npts):
@@ -128,7 +136,8 @@ def _run(world, bs, npts):
     port = _port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, bs, npts, q)) for r in range(world)]
     old = os.environ.get("GPU_MAX_HW_QUEUES")
-    os.environ["GPU_MAX_HW_QUEUES"] = RANK_HW_QUEUES     # inherited by the spawned ranks only
+    if RANK_HW_QUEUES != "default":
+        os.environ["GPU_MAX_HW_QUEUES"] = RANK_HW_QUEUES     # inherited by the spawned ranks only
     try:
         for p in procs:
             p.start()

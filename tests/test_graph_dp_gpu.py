@@ -74,6 +74,7 @@ def _worker(rank, world, port, sync_bn, q):
             eager_orders.append(list(b.reducer.issued))
             same_loss &= bool(torch.equal(la, lb))
         res["orders"], res["eager_orders"], res["nbuckets"] = orders, eager_orders, a.reducer.num_buckets
+        res["deferred"] = list(a.reducer.deferred)
         ent = next(iter(g.graphs.values()))
         res["segments"], res["collectives"] = len(ent[1].graphs), len(ent[1].collectives)
         res["ngraphs"] = len(g.graphs)
@@ -122,7 +123,8 @@ def test_graph_dp_replay_equals_eager(dev, sync_bn):
         assert "error" not in r, r.get("error")
     for r in res:
         print(f"rank {r['rank']}: {r['ngraphs']} graph(s), {r['segments']} segments / {r['collectives']} "
-              f"collectives, {r['n_tensors']} tensors compared")
+              f"collectives, {r['nbuckets']} buckets, {len(r['deferred'])} bucket hooks off the capture stream, "
+              f"{r['n_tensors']} tensors compared")
         assert r["ngraphs"] == 1
         assert r["collectives"] >= 1 and r["segments"] == r["collectives"] + 1
         # the gradient buckets are all-reduced from the replayed step, between its backward

@@ -84,7 +84,7 @@ def _worker(port, q):
         g1 = GraphedStep(make(DataParallelStep, dict(cfg1, **force)))
         l_g1, p_g1 = run(g1), params(g1)
         ent = next(iter(g1.graphs.values()))
-        res["inline"] = bool(ent[3]) and len(ent[1].graphs) == 1 and not ent[1].collectives
+        res["inline"] = ent[1].inline and bool(ent[3]) and len(ent[1].graphs) == 1 and not ent[1].collectives
         res["buckets"] = g1.inner.reducer.num_buckets
         res["eager1_eq_train"] = l_e1 == l_ref1 and all(torch.equal(p_e1[k], p_ref1[k]) for k in p_ref1)
         res["graph1_eq_train"] = l_g1 == l_ref1 and all(torch.equal(p_g1[k], p_ref1[k]) for k in p_ref1)
@@ -95,14 +95,16 @@ def _worker(port, q):
         res["graph2_eq_eager2"] = l_g2 == l_e2 and all(torch.equal(p_g2[k], p_e2[k]) for k in p_e2)
         res["contrast_rel"] = [abs(a - b) / abs(b) for a, b in zip(l_e2, l_ref2)]
         # the world > 1 default: segmented capture, RCCL collectives eagerly between the graph
-        # segments and the gradient all-reduce after the replay (forced here at world size 1)
+        # segments — the all_gather and each gradient bucket's all-reduce, issued from the
+        # replayed backward between its segments (forced here at world size 1)
         seg = {"graph_inline_collectives": False}
         g3 = GraphedStep(make(DataParallelStep, dict(cfg1, **force, **seg)))
         l_g3, p_g3 = run(g3), params(g3)
         g4 = GraphedStep(make(DataParallelStep, dict(cfg2, **force, **seg)))
         l_g4, p_g4 = run(g4), params(g4)
         ent4 = next(iter(g4.graphs.values()))
-        res["segmented"] = not ent4[3] and len(ent4[1].graphs) == len(ent4[1].collectives) + 1 >= 2
+        res["segmented"] = (not ent4[1].inline and bool(ent4[3])
+                            and len(ent4[1].graphs) == len(ent4[1].collectives) + 1 >= 3)
         res["seg1_eq_train"] = l_g3 == l_ref1 and all(torch.equal(p_g3[k], p_ref1[k]) for k in p_ref1)
         res["seg2_eq_eager2"] = l_g4 == l_e2 and all(torch.equal(p_g4[k], p_e2[k]) for k in p_e2)
         res["losses"] = (l_ref1[:2], l_e1[:2], l_g1[:2])
