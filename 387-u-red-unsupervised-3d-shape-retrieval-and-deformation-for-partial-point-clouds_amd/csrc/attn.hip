@@ -13,6 +13,7 @@
 // rows padded to d+1 floats so the per-(i, j) dot products (consecutive threads on
 // consecutive key rows) are bank-conflict free. fp32 throughout, fixed summation order
 // (deterministic).
+#define URED_DBG_FILE 6
 #include "ured_common.h"
 #include "ured_hip.h"
 
@@ -201,3 +202,5 @@ int ured_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float*
 }
 
 }  // extern "C"
+
+URED_DBG_ACCESSOR(ured_dbg_attn)

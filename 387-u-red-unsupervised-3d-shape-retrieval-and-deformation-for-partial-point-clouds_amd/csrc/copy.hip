@@ -6,6 +6,7 @@
 // its two addresses and size allow); the launch's threads stride over the concatenated unit
 // ranges, so a large item and many small ones share the grid.
 #include <hip/hip_runtime.h>
+#define URED_DBG_FILE 7
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -61,3 +62,5 @@ extern "C" int ured_copy_batch(const UredCopyItem* items, int n, void* stream) {
     hipLaunchKernelGGL(copy_batch_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
     return ured::launch_status("ured_copy_batch");
 }
+
+URED_DBG_ACCESSOR(ured_dbg_copy)

@@ -23,6 +23,7 @@
 // objects staged through LDS as SoA + price (broadcast reads). Workgroups whose 64 bidders are
 // all assigned leave at once, so late iterations cost little. Backward is a gather (each point
 // owns its gradient): no atomics.
+#define URED_DBG_FILE 5
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -218,3 +219,5 @@ int ured_emd_bwd(const float* xyz1, const float* xyz2, int b, int n, const float
 }
 
 }  // extern "C"
+
+URED_DBG_ACCESSOR(ured_dbg_emd)

@@ -26,6 +26,7 @@
 // stored and read back write-through, see last_arrival), in a fixed order, in fp64. The counter is reset by that
 // workgroup, so a launch leaves it at 0 for the next one (and for HIP-graph replays).
 #include <hip/hip_runtime.h>
+#define URED_DBG_FILE 3
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -128,8 +129,9 @@ __global__ __launch_bounds__(LT) void cd_pair_prep_kernel(CdShape sh, const floa
             reinterpret_cast<int4*>(segf)[s] = q;
         } else {
             const bool v = i < kb;
-            URED_DBG_CHECK(!v || (off[b * sh.P + i] >= 0 && counts[(size_t)b * sh.P + i] >= 0 &&
-                                  off[b * sh.P + i] + counts[(size_t)b * sh.P + i] <= sh.N));
+            // off: the part's first row in the [B * N] sorted rows (b * N + start, csrc/parts.hip)
+            URED_DBG_CHECK(!v || (off[b * sh.P + i] >= b * sh.N && counts[(size_t)b * sh.P + i] >= 0 &&
+                                  off[b * sh.P + i] + counts[(size_t)b * sh.P + i] <= (long long)(b + 1) * sh.N));
             int4 q = make_int4(s * sh.S + i * sh.NP, v ? sh.NP : 0, off[b * sh.P + i] + h * (int)BN,
                                v ? (int)counts[(size_t)b * sh.P + i] : 0);
             reinterpret_cast<int4*>(segp)[s * sh.P + i] = q;
@@ -162,7 +164,8 @@ __global__ __launch_bounds__(LT) void cd_pair_reduce_kernel(CdShape sh, const fl
             float s0 = 0.f, s1 = 0.f;
             for (int p = t; p < sh.NP; p += LT) { s0 += daf[a0 + p]; s1 += dap[a0 + p]; }
             const int cnt = (int)counts[(size_t)b * sh.P + i];
-            URED_DBG_CHECK(kb <= sh.P && cnt >= 0 && off[b * sh.P + i] >= 0 && off[b * sh.P + i] + cnt <= sh.N);
+            URED_DBG_CHECK(kb <= sh.P && cnt >= 0 && off[b * sh.P + i] >= b * sh.N &&
+                           off[b * sh.P + i] + cnt <= (b + 1) * sh.N);
             const long long b0 = (long long)off[b * sh.P + i] + (long long)h * sh.B * sh.N;
             float s2 = 0.f;
             for (int j = t; j < cnt; j += LT) s2 += dbp[b0 + j];
@@ -710,3 +713,5 @@ int ured_loss_assemble_bwd(int K, const float* weights, const float* g, float* g
 }
 
 }  // extern "C"
+
+URED_DBG_ACCESSOR(ured_dbg_loss)

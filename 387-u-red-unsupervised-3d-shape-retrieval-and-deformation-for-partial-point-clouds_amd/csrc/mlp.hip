@@ -25,6 +25,7 @@
 //    BN-backward masks/partials of the previous layer, or split-K partials;
 //  * XCD-aware tile order: blocks that share an A row-panel run on one XCD.
 #include <cstdlib>
+#define URED_DBG_FILE 1
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -220,11 +221,8 @@ __host__ __device__ __forceinline__ size_t part_idx(int q, int col, int blk, int
     return ((size_t)q * N + col) * nblk + blk;
 }
 
-// Debug build (-DURED_DEBUG_BOUNDS=1): every LDS-DMA destination range and every epilogue
-// buffer-store offset is checked against its allocation on the device (trap on violation).
-#ifndef URED_DEBUG_BOUNDS
-#define URED_DEBUG_BOUNDS 0
-#endif
+// Debug build (-DURED_DEBUG_BOUNDS=1, ured_common.h): every LDS-DMA destination range and every
+// epilogue buffer-store offset is checked against its allocation on the device.
 
 // Phase timing build (-DURED_GEMM_TIMING=1 -DURED_TS_M=.. -DURED_TS_N=.. -DURED_TS_K=..): the
 // BN-backward dgrad launches of that shape record, per workgroup, the real-time clock (100 MHz) at
@@ -289,7 +287,7 @@ struct OutTile {
             // 32-bit byte offset (buf_ok guarantees M * ld * 4 < 2^31) and a select: no branch
             const unsigned off = (unsigned)row * ld4 + (unsigned)col * 4u;
 #if URED_DEBUG_BOUNDS
-            if (ok && (row < 0 || col < 0 || off + 4u > nrec)) __builtin_trap();
+            URED_DBG_CHECK(!(ok && (row < 0 || col < 0 || off + 4u > nrec)));
 #endif
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc, ok ? off : ST_OOB, 0, 0);
         } else if (ok) {
@@ -399,8 +397,8 @@ __device__ __forceinline__ void bnbwd_full(const UredGemmDesc& d, f16v (&acc)[2]
                     xh = (y - mu_[j]) * is_[j];
                 }
 #if URED_DEBUG_BOUNDS
-                if ((unsigned long long)vo + roff(i, r, lc) + 4u > (unsigned long long)(((long long)(d.M - 1) * d.ldc + d.N) * 4) ||
-                    r0 + (unsigned)(i * 32 + (r & 3) + 8 * (r >> 2)) >= (unsigned)d.M) __builtin_trap();
+                URED_DBG_CHECK(!((unsigned long long)vo + roff(i, r, lc) + 4u > (unsigned long long)(((long long)(d.M - 1) * d.ldc + d.N) * 4) ||
+                                 r0 + (unsigned)(i * 32 + (r & 3) + 8 * (r >> 2)) >= (unsigned)d.M));
 #endif
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, g), cr, vo, roff(i, r, lc), 0);
                 a1 += g;
@@ -916,7 +914,7 @@ template <bool KM, int NP>
 __device__ __forceinline__ void buf_tile(const BufOperand& o, int ld, int k0, float* smem, unsigned off) {
     const unsigned toff = KM ? (unsigned)k0 * (unsigned)ld * 4u : (unsigned)k0 * 4u;
 #if URED_DEBUG_BOUNDS
-    if (off + NP * 1024u > GEMM2_SMEM_BYTES || (off & 1023u)) __builtin_trap();
+    URED_DBG_CHECK(!(off + NP * 1024u > GEMM2_SMEM_BYTES || (off & 1023u)));
 #endif
     char* base = reinterpret_cast<char*>(smem) + off;
 #pragma unroll
@@ -2059,3 +2057,5 @@ int ured_debug_gemm_ts_clear() {
 }
 #endif
 }  // extern "C"
+
+URED_DBG_ACCESSOR(ured_dbg_mlp)

@@ -24,6 +24,7 @@
 //   output; the contributions of the other direction are found by streaming the
 //   other side's idx array through LDS in ascending order, each wave compacting
 //   the entries that target its own 64 points (O(n + m) work per pair).
+#define URED_DBG_FILE 2
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -1039,3 +1040,5 @@ int ured_dcd(const float* dist1, const int* idx1, const float* dist2, const int*
 }
 
 }  // extern "C"
+
+URED_DBG_ACCESSOR(ured_dbg_nn)

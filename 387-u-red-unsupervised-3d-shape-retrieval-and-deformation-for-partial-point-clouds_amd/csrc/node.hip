@@ -20,6 +20,7 @@
 // The epilogue fuses bias, a per-row-group bias (param_decoder's broadcast global half),
 // ReLU, a ReLU gate (backward mask), a residual add and accumulation.
 #include <hip/hip_runtime.h>
+#define URED_DBG_FILE 4
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -721,3 +722,5 @@ int ured_debug_node_ts(unsigned long long* host, int n) {
 }
 #endif
 }  // extern "C"
+
+URED_DBG_ACCESSOR(ured_dbg_node)

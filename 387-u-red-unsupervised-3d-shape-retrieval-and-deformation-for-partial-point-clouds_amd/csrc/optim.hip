@@ -19,6 +19,7 @@
 //   g += wd * p;  m = b1*m + (1-b1)*g;  v = b2*v + (1-b2)*g*g;
 //   step_size = lr / (1 - b1^t);  denom = sqrt(v) / sqrt(1 - b2^t) + eps;  p -= step_size * m / denom
 #include <hip/hip_runtime.h>
+#define URED_DBG_FILE 8
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -138,3 +139,5 @@ int ured_adam_clip_step(float* param, float* grad, float* exp_avg, float* exp_av
 }
 
 }  // extern "C"
+
+URED_DBG_ACCESSOR(ured_dbg_optim)

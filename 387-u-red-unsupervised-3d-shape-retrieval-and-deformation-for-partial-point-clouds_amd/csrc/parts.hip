@@ -12,6 +12,7 @@
 //     order-independent, so the box is exact) and param_def indexed by label value
 //     (engine/train.py:120: param_def[w, int(sem)] = compute_aabbox(part points)).
 #include <hip/hip_runtime.h>
+#define URED_DBG_FILE 9
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -139,3 +140,5 @@ extern "C" int ured_build_parts(const long long* labels, const float* x, int B, 
                        perm, inv_perm, gid, off, counts, k, mask, rank_of_label, present, aabb, param_def);
     return ured::launch_status("ured_build_parts");
 }
+
+URED_DBG_ACCESSOR(ured_dbg_parts)

@@ -15,6 +15,7 @@
 // Partial layout (mlp.hip part_idx): [q][column][row block], row blocks of 128 rows; group_w
 // (nullable) gives the row multiplicity of a unique-row batch per group of group_rows rows.
 #include <hip/hip_runtime.h>
+#define URED_DBG_FILE 10
 #include "ured_common.h"
 #include "../../include/ured_hip.h"
 
@@ -174,3 +175,5 @@ int ured_bn_bwd_finalize_sums(const double* local, const double* global, int N, 
 }
 
 }  // extern "C"
+
+URED_DBG_ACCESSOR(ured_dbg_syncbn)

@@ -32,16 +32,40 @@ inline int launch_status(const char* what) {
 }  // namespace ured
 
 // Debug build (-DURED_DEBUG_BOUNDS=1): device-side bounds checks of the indices a kernel derives
-// from its arguments or reads from device tables (segment tables, NN indices, labels), and of the
-// raw buffer offsets of the MFMA kernels; a violation traps (the launch fails with a fault that
-// names the kernel). Compiled out (no code) in the default build.
+// from its arguments or reads from device tables (segment tables, NN indices, labels), of the raw
+// buffer offsets and LDS-DMA ranges of the MFMA kernels, and of their epilogue stores. A violation
+// does not trap: the first one of each source file is recorded as (file id << 32 | line) in that
+// file's device word, which the host reads (and clears) through ured_debug_violation(file id)
+// (tests/conftest.py checks it after every test when the debug library is loaded). Compiled out
+// (no code) in the default build.
 #ifndef URED_DEBUG_BOUNDS
 #define URED_DEBUG_BOUNDS 0
 #endif
-#define URED_DBG_CHECK(cond)                                     \
-    do {                                                         \
-        if (URED_DEBUG_BOUNDS && !(cond)) __builtin_trap();      \
+#if URED_DEBUG_BOUNDS
+#ifndef URED_DBG_FILE
+#error "define URED_DBG_FILE (the source file's id) before including ured_common.h"
+#endif
+__device__ unsigned long long ured_dbg_first;   // one per source file (each .hip is its own code object)
+#define URED_DBG_CHECK(cond)                                                                             \
+    do {                                                                                                 \
+        if (!(cond))                                                                                     \
+            atomicCAS(&ured_dbg_first, 0ull, ((unsigned long long)URED_DBG_FILE << 32) | (unsigned)__LINE__); \
     } while (0)
+// host accessor of this file's word (one extern "C" function per source file)
+#define URED_DBG_ACCESSOR(NAME)                                                                          \
+    extern "C" unsigned long long NAME(int reset) {                                                      \
+        unsigned long long v = 0;                                                                        \
+        if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(ured_dbg_first), sizeof v) != hipSuccess) return ~0ull;   \
+        if (reset) {                                                                                     \
+            const unsigned long long z = 0;                                                              \
+            if (hipMemcpyToSymbol(HIP_SYMBOL(ured_dbg_first), &z, sizeof z) != hipSuccess) return ~0ull; \
+        }                                                                                                \
+        return v;                                                                                        \
+    }
+#else
+#define URED_DBG_CHECK(cond) do { } while (0)
+#define URED_DBG_ACCESSOR(NAME)
+#endif
 
 #define URED_REQUIRE(cond, ...)                                  \
     do {                                                         \

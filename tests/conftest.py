@@ -42,3 +42,32 @@ def pytest_collection_modifyitems(session, config, items):
         r = _LAST.get(os.path.basename(str(item.fspath)), 0)
         return (r, "eight_ranks" in item.name)
     items[:] = sorted(items, key=rank)       # stable: the default order otherwise
+
+
+# The bounds-checked debug build (-DURED_DEBUG_BOUNDS=1, loaded through URED_LIB; tools/
+# debug_bounds_suite.sh) records the first violated device-side check of each source file instead of
+# trapping; after every GPU test the words are read (and cleared) and a violation fails the test
+# with the file and line of the check.
+_DBG_FILES = {1: "mlp.hip", 2: "nn.hip", 3: "loss.hip", 4: "node.hip", 5: "emd.hip", 6: "attn.hip",
+              7: "copy.hip", 8: "optim.hip", 9: "parts.hip", 10: "syncbn.hip"}
+
+
+@pytest.fixture(autouse=True)
+def _debug_bounds_violations(request):
+    yield
+    mod = sys.modules.get("ured_hip._lib")
+    if "gpu" not in request.keywords or mod is None or mod._lib is None:
+        return
+    import ctypes
+    found = []
+    for name in ("mlp", "nn", "loss", "node", "emd", "attn", "copy", "optim", "parts", "syncbn"):
+        fn = getattr(mod._lib, "ured_dbg_" + name, None) if hasattr(mod._lib, "ured_dbg_" + name) else None
+        if fn is None:
+            return                              # not the debug build
+        fn.restype, fn.argtypes = ctypes.c_ulonglong, [ctypes.c_int]
+        import torch
+        torch.cuda.synchronize()
+        v = fn(1)
+        if v:
+            found.append(f"{_DBG_FILES.get(v >> 32, v >> 32)}:{v & 0xFFFFFFFF}")
+    assert not found, "device-side bounds check violated (debug build): " + ", ".join(found)
