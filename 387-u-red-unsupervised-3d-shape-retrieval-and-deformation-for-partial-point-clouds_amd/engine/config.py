@@ -42,7 +42,7 @@ EXTRA = {
     "unique_sources", "flat_adam", "fused_adam", "cuda_graph",
     "log_every", "compute_connectivity", "src_connectivity_plane", "synthetic_targets", "differentiable_gather", "sync_bn", "loss_head", "dist_backend",
     # data parallel (engine/dp.py, engine/graph.py)
-    "dp_last_bucket_mb", "dp_force_collectives", "graph_inline_collectives",
+    "dp_bucket_mb", "dp_last_bucket_mb", "dp_force_collectives", "graph_inline_collectives",
 }
 
 TRAIN_REQUIRED = ("source_latent_dim", "target_latent_dim", "sem_latent_dim", "MAX_NUM_PARTS", "device",

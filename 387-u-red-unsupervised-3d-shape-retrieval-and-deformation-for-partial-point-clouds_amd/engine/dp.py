@@ -304,7 +304,7 @@ class DataParallelStep(TrainStep):
     contrastive all_gather) through the process group even at world size 1 — the test hook that
     exercises the RCCL code paths, eager and captured, on a one-GPU box."""
 
-    def __init__(self, cfg, db, device, bucket_mb=25.0, overlap=None, last_bucket_mb=None):
+    def __init__(self, cfg, db, device, bucket_mb=None, overlap=None, last_bucket_mb=None):
         super().__init__(cfg, db, device)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.collect = self.world > 1 or (bool(cfg.get("dp_force_collectives", False)) and dist.is_initialized())
@@ -315,6 +315,8 @@ class DataParallelStep(TrainStep):
         for name in CLIPPED:
             params += [p for p in self.models[name].parameters() if p.requires_grad]
         self.params = params[::-1]          # ~ the order backward produces gradients
+        if bucket_mb is None:
+            bucket_mb = cfg.get("dp_bucket_mb", 25.0)
         self.bucket_elems = int(bucket_mb * 1e6 / 4)
         self._buckets = None                # torch-Adam path: (active key, buckets)
         overlap = self.collect if overlap is None else bool(overlap)

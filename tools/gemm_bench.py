@@ -1,6 +1,6 @@
 """Micro-benchmark of ured_gemm on the U-RED step's dominant layer shapes (config 2).
 
-  python tools/gemm_bench.py [--iters 20]
+  python tools/gemm_bench.py [--iters 20] [--step] [--lib]
 Prints TFLOP/s per (shape, variant); interleaves variants in one process (rule 24).
 """
 import argparse
@@ -51,6 +51,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--step", action="store_true", help="the config-2 step's layer sizes instead of M=262144")
+    ap.add_argument("--lib", action="store_true",
+                    help="also time torch.mm (the ROCm BLAS library, fp32) on the same plain products")
     ap.add_argument("--dgrad-layouts", action="store_true",
                     help="also time store-only dgrad with the weight k-major vs pre-transposed (row-major)")
     a = ap.parse_args()
@@ -87,6 +89,15 @@ def main():
             r["dgrad_store_T"] = flop / timeit(lambda: K.gemm(M, Kd, N, dY, N, Wt, N, G, Kd), a.iters) / 1e12
         r["wgrad"] = flop / timeit(lambda: K.wgrad(dY, N, X, Kd, N, Kd, M, dW, Kd, pro=K.PRO_ENC, pro_s=s, pro_t=t),
                                    a.iters) / 1e12
+        if a.lib:
+            torch.backends.cuda.matmul.allow_tf32 = False
+            Yl = torch.empty(M, N, device=dev)
+            Gl = torch.empty(M, Kd, device=dev)
+            dWl = torch.empty(N, Kd, device=dev)
+            r["lib_fwd"] = flop / timeit(lambda: torch.mm(X, W.t(), out=Yl), a.iters) / 1e12
+            r["lib_dgrad"] = flop / timeit(lambda: torch.mm(dY, W, out=Gl), a.iters) / 1e12
+            r["lib_wgrad"] = flop / timeit(lambda: torch.mm(dY.t(), X, out=dWl), a.iters) / 1e12
+            del Yl, Gl, dWl
         out[name] = {k: round(v, 1) for k, v in r.items()}
         print(name, out[name], flush=True)
         del X, W, Y, ws, dY, G, bws, dW
