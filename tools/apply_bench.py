@@ -52,13 +52,14 @@ def main():
         ca, cb, cc = (torch.randn(N, device=dev, generator=g) for _ in range(3))
         st = _lib.stream_of(Y)
 
-        def apply(res=0):
+        def apply(res=0, colsum=True):
             _lib.call("ured_bn_bwd_apply", K._p(G), K._p(Y), M, N, N, res, K._p(mean), K._p(ca), K._p(cb),
-                      K._p(cc), K._p(dY), K._p(cs), None, 0, st)
+                      K._p(cc), K._p(dY), K._p(cs) if colsum else None, None, 0, st)
 
         byts = 3.0 * M * N * 4
         r = {"apply": byts / timeit(apply, a.iters) / 1e9,
              "apply_res": byts / timeit(lambda: apply(1), a.iters) / 1e9,
+             "apply_no_colsum": byts / timeit(lambda: apply(0, False), a.iters) / 1e9,
              "torch_add": byts / timeit(lambda: torch.add(G, Y, out=dY), a.iters) / 1e9,
              "torch_copy(2x traffic/3)": 2.0 * M * N * 4 / timeit(lambda: dY.copy_(G), a.iters) / 1e9}
         name = f"{M}x{N}"
