@@ -601,9 +601,11 @@ def trainable(params):
 # inference (engine/vis.py:118-256, batched)
 # ----------------------------------------------------------------------------
 
-def infer(params, batch, cfg, chunk=512):
+def infer(params, batch, cfg, chunk=512, retrieved=None):
     """Retrieval + deformation in eval mode. batch holds src_points/src_mats/src_sem (the whole DB),
-    x, labels, tgt_sem. Returns retrieved [B,P] (-1 for empty slots), top-2 gap, params, out, cd [B]."""
+    x, labels, tgt_sem. Returns retrieved [B,P] (-1 for empty slots), top-2 gap, the similarity
+    matrix [B,P,S], params, out, cd [B]. retrieved (optional, [B,P]): deform these sources instead
+    of the argmax (the test deforms the GPU's picks where a near-tie flipped one)."""
     with torch.no_grad():
         emb = params["embedding_layer"]["weight"]
         pts, sem = batch["src_points"], batch["src_sem"]
@@ -620,10 +622,13 @@ def infer(params, batch, cfg, chunk=512):
         part_f, _, mask, _, _ = get_part(pp.permute(0, 2, 1), batch["labels"], x, P)
         sim = F.normalize(part_f, dim=-1, p=2) @ codes.t()
         top2 = sim.topk(2, dim=-1).values
-        retrieved = torch.where(mask > 0, sim.argmax(-1), torch.full((B, P), -1, dtype=torch.long))
+        if retrieved is None:
+            retrieved = torch.where(mask > 0, sim.argmax(-1), torch.full((B, P), -1, dtype=torch.long))
+        else:
+            retrieved = torch.where(mask > 0, retrieved.long(), torch.full((B, P), -1, dtype=torch.long))
         idx = torch.where(retrieved < 0, retrieved + pts.shape[0], retrieved)
         prm = deform_net(params["param_decoder_full"], tcode, codes[idx], training=False)
         out = get_shape(batch["src_mats"][idx], prm, torch.zeros_like(prm), cfg["alpha"]).reshape(B, -1, 3)
         cd = chamfer_distance2(out, x)
-        return {"retrieved": retrieved, "sim_top2_gap": top2[..., 0] - top2[..., 1], "params": prm,
+        return {"retrieved": retrieved, "sim_top2_gap": top2[..., 0] - top2[..., 1], "sim": sim, "params": prm,
                 "out": out, "cd": cd}

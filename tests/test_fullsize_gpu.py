@@ -214,8 +214,10 @@ def test_config5_train_step_4096_points(dev):
 @pytest.mark.timeout(900)
 def test_config3_inference_full_size(dev):
     """engine/test.py inference at bs=16, 2048 points, C=512 over 512 sources vs ured_ref.infer
-    (float64). Retrieval indices bit-exact outside top-2 gaps < 1e-6; chamfer and DeformNet
-    params of the samples whose retrieval agrees on every part within 1e-4 / 1e-3."""
+    (float64). Retrieval indices bit-exact outside top-2 gaps < 1e-6, and where a near-tie flipped
+    a pick, the GPU's source is within 1e-6 of the float64 maximum similarity. Chamfer and
+    DeformNet params of EVERY sample within 1e-4 / 1e-3: the oracle deforms the GPU's picks
+    (ured_ref.infer(retrieved=...)), so a flipped near-tie is compared too, not skipped."""
     from dataset import synthetic
     from train_utils.load_sources import SourceDB
     from engine.train import get_models, batch_to_device
@@ -245,11 +247,15 @@ def test_config3_inference_full_size(dev):
     flips = int(((got != ref) & near).sum())
     step_parity.report(f"\nconfig3: {int(valid.sum())} retrievals, {int(near.sum())} near-ties (gap < 1e-6), {flips} flipped")
     assert int(mism.sum()) == 0, f"{int(mism.sum())} retrieval mismatches outside near-ties"
-    same = (got == ref).all(dim=1)
-    assert int(same.sum()) >= 12
-    np.testing.assert_allclose(r["cd"].cpu()[same].double().numpy(), R["cd"][same].numpy(), rtol=1e-4)
-    np.testing.assert_allclose(r["params"].cpu()[same].double().numpy(), R["params"][same].numpy(),
-                               rtol=1e-3, atol=1e-5)
+    # a flipped pick is a near-optimal source in float64 terms
+    sim = R["sim"]
+    pick = sim.gather(-1, got.clamp(min=0).long().unsqueeze(-1)).squeeze(-1)
+    loss_of_pick = (sim.max(-1).values - pick)[valid]
+    assert float(loss_of_pick.max()) < 1e-6, f"a GPU pick is {float(loss_of_pick.max()):.3e} below the best similarity"
+    # deformation of the GPU's picks, every sample
+    R2 = R if flips == 0 else ured_ref.infer(P64, ob, cfg, retrieved=got)
+    np.testing.assert_allclose(r["cd"].cpu().double().numpy(), R2["cd"].numpy(), rtol=1e-4)
+    np.testing.assert_allclose(r["params"].cpu().double().numpy(), R2["params"].numpy(), rtol=1e-3, atol=1e-5)
 
 
 @pytest.mark.timeout(600)
