@@ -1,6 +1,6 @@
 # Full check on one box: the whole GPU suite once (-x, multi-process rehearsals last), smoke,
-# the default bench line, then a whole-step A/B of the DMA issue point (in-tree: ahead of the
-# MFMAs; B: among them).
+# the default bench line, then (AB=<lib.so>) a whole-step A/B of the in-tree library against
+# that build.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
