@@ -10,15 +10,19 @@ kernel each way (ured_hip.attn), out_proj as a node GEMM, and the FeedForwardNet
 BatchNorm kernel, the concatenation [x, message] read in place. `forward` keeps the
 reference's channel-first signature for drop-in callers.
 """
+import os
+
 import torch
 import torch.nn as nn
 
-from ured_hip.attn import cross_attention, self_attention
+from ured_hip.attn import cross_attention, self_attention, self_attention_pair
 from ured_hip.node import node_ffn, node_linear, node_proj
 
 from . import get_attention_mechanism
 from .attention import softmax_attention
 from .attention_utils import FeedForwardNet_norm, conv1x1
+
+_ATTN_PAIR = os.environ.get("URED_ATTN_PAIR", "1") == "1"     # A/B knob (tools/gpu_py_ab.sh)
 
 
 class MultiheadAttention(nn.Module):
@@ -98,9 +102,10 @@ class ResidualAttentionMessagePropagation(nn.Module):
     def forward_nodes_self_pair(self, x0, x1):
         """(forward_nodes(x0), forward_nodes(x1)) — the two self-attention calls of a
         DescriptorsSelfAttention layer (shared weights) — with every node GEMM run once over
-        the rows of both node sets: the attention and the BatchNorm still see one set at a
-        time (per-set batch statistics, running stats updated set 0 then set 1), so the values
-        are those of the two calls; half the launches, no gradient accumulation across calls."""
+        the rows of both node sets, and both sets' attention in one launch (ured_hip.attn
+        SelfAttnPairFn): the attention and the BatchNorm still see one set at a time (per-set
+        batch statistics, running stats updated set 0 then set 1), so the values are those of the
+        two calls; half the launches, no gradient accumulation across calls."""
         mha = self.mha
         if mha.attention_func is not softmax_attention or not self._node_ffn_ok():
             return self.forward_nodes(x0), self.forward_nodes(x1)
@@ -110,9 +115,13 @@ class ResidualAttentionMessagePropagation(nn.Module):
         X = torch.cat([x0.reshape(R0, C), x1.reshape(R1, C)])
         q_, k_, v_ = mha.in_proj_q, mha.in_proj_k, mha.in_proj_v
         qkv = node_proj((X,), [(mha._w(q_), mha._w(k_), mha._w(v_))], [(q_.bias, k_.bias, v_.bias)])
-        q0, q1 = qkv.split([R0, R1])
-        o = torch.cat([self_attention(q0.view(B, n0, -1), mha.num_heads).reshape(R0, C),
-                       self_attention(q1.view(B, n1, -1), mha.num_heads).reshape(R1, C)])
+        if _ATTN_PAIR:
+            # both sets' attention in one launch each way, reading / writing row blocks of qkv / o
+            o = self_attention_pair(qkv, B, n0, n1, mha.num_heads)
+        else:
+            q0, q1 = qkv.split([R0, R1])
+            o = torch.cat([self_attention(q0.view(B, n0, -1), mha.num_heads).reshape(R0, C),
+                           self_attention(q1.view(B, n1, -1), mha.num_heads).reshape(R1, C)])
         message = node_linear(o, mha._w(mha.out_proj), mha.out_proj.bias)
         first, R = (X - message, X) if self.use_offset else (X, None)
         out0, out1 = node_ffn(self.fc, first, message, R, (0, R0, R0 + R1)).split([R0, R1])

@@ -35,6 +35,24 @@ struct AttnArgs {
     float* dv; int lddv;
 };
 
+// Up to URED_ATTN_MAX_SETS independent calls per launch: set si owns workgroups
+// [first[si], first[si + 1]), one per (sample, head) of that call, so each block computes exactly what
+// a separate launch's block would.
+struct AttnSets {
+    AttnArgs s[URED_ATTN_MAX_SETS];
+    int first[URED_ATTN_MAX_SETS + 1];
+    int nsets;
+};
+
+__device__ __forceinline__ const AttnArgs& pick_set(const AttnSets& S, int& bx) {
+    int si = 0;
+#pragma unroll
+    for (int q = 1; q < URED_ATTN_MAX_SETS; ++q)
+        if (q < S.nsets && (int)blockIdx.x >= S.first[q]) si = q;
+    bx = (int)blockIdx.x - S.first[si];
+    return S.s[si];
+}
+
 // Load rows x (row stride ld, head offset h*d) of `rows` nodes into LDS [rows][d+1]: 16-B global
 // loads when the head slice is 16-B aligned (the fused projection outputs are), else 4-B loads.
 __device__ inline void load_rows(float* dst, const float* src, int ld, int rows, int d, int hoff, int b) {
@@ -55,9 +73,11 @@ __device__ inline void load_rows(float* dst, const float* src, int ld, int rows,
     }
 }
 
-__global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(const AttnSets sets) {
     extern __shared__ float sm[];
-    const int b = blockIdx.x / a.H, h = blockIdx.x - b * a.H;
+    int bx;
+    const AttnArgs& a = pick_set(sets, bx);
+    const int b = bx / a.H, h = bx - b * a.H;
     const int n = a.n, m = a.m, d = a.d, dp = d + 1, hoff = h * d;
     float* Q = sm;
     float* Kt = Q + n * dp;
@@ -74,7 +94,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnArgs a) {
         S[e] = s * a.scale;
     }
     __syncthreads();
-    float* W = a.w + (size_t)blockIdx.x * n * m;
+    float* W = a.w + (size_t)bx * n * m;
     for (int i = threadIdx.x; i < n; i += ATT_THREADS) {
         float mx = -__builtin_inff();
         for (int j = 0; j < m; ++j) mx = fmaxf(mx, S[i * m + j]);
@@ -100,9 +120,11 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(AttnArgs a) {
     }
 }
 
-__global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(const AttnSets sets) {
     extern __shared__ float sm[];
-    const int b = blockIdx.x / a.H, h = blockIdx.x - b * a.H;
+    int bx;
+    const AttnArgs& a = pick_set(sets, bx);
+    const int b = bx / a.H, h = bx - b * a.H;
     const int n = a.n, m = a.m, d = a.d, dp = d + 1, hoff = h * d;
     float* Q = sm;
     float* Kt = Q + n * dp;
@@ -114,7 +136,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(AttnArgs a) {
     load_rows(Kt, a.k, a.ldk, m, d, hoff, b);
     load_rows(V, a.v, a.ldv, m, d, hoff, b);
     load_rows(dO, a.dout, a.lddo, n, d, hoff, b);
-    const float* W = a.w + (size_t)blockIdx.x * n * m;
+    const float* W = a.w + (size_t)bx * n * m;
     for (int e = threadIdx.x; e < n * m; e += ATT_THREADS) P[e] = W[e];
     __syncthreads();
     // dV[j][c] = sum_i P[i][j] dO[i][c]
@@ -166,6 +188,49 @@ int check_sizes(const char* who, int B, int H, int n, int m, int d) {
 size_t fwd_lds(int n, int m, int d) { return sizeof(float) * ((size_t)(n + 2 * m) * (d + 1) + (size_t)n * m); }
 size_t bwd_lds(int n, int m, int d) { return sizeof(float) * ((size_t)(2 * n + 2 * m) * (d + 1) + 2 * (size_t)n * m); }
 
+
+// Validate one set and add it to the launch table (B == 0 sets add no workgroups).
+int add_set(const char* who, bool bwd, const UredAttnSet& x, AttnSets& S, size_t& lds) {
+    if (int rc = check_sizes(who, x.B, x.H, x.n, x.m, x.d)) return rc;
+    const size_t need = bwd ? bwd_lds(x.n, x.m, x.d) : fwd_lds(x.n, x.m, x.d);
+    URED_REQUIRE(need <= 65536, "%s: n=%d m=%d d=%d needs more than 64 KB of LDS", who, x.n, x.m, x.d);
+    if (x.B == 0) return 0;
+    const int hd = x.H * x.d;
+    URED_REQUIRE(x.q && x.k && x.v && x.weights, "%s: null pointer", who);
+    URED_REQUIRE(x.ldq >= hd && x.ldk >= hd && x.ldv >= hd, "%s: row stride < H*d", who);
+    if (bwd) {
+        URED_REQUIRE(x.dout && x.dq && x.dk && x.dv, "%s: null pointer", who);
+        URED_REQUIRE(x.lddo >= hd && x.lddq >= hd && x.lddk >= hd && x.lddv >= hd, "%s: row stride < H*d", who);
+    } else {
+        URED_REQUIRE(x.out, "%s: null pointer", who);
+        URED_REQUIRE(x.ldo >= hd, "%s: row stride < H*d", who);
+    }
+    const long long end = (long long)S.first[S.nsets] + (long long)x.B * x.H;
+    URED_REQUIRE(end <= 0x7fffffffLL, "%s: too many (sample, head) pairs", who);
+    S.s[S.nsets] = AttnArgs{x.q, x.ldq, x.k, x.ldk, x.v, x.ldv, x.n, x.m, x.d, x.H, x.scale,
+                            bwd ? nullptr : x.out, bwd ? 0 : x.ldo, x.weights, bwd ? x.dout : nullptr,
+                            bwd ? x.lddo : 0, bwd ? x.dq : nullptr, bwd ? x.lddq : 0, bwd ? x.dk : nullptr,
+                            bwd ? x.lddk : 0, bwd ? x.dv : nullptr, bwd ? x.lddv : 0};
+    S.first[S.nsets + 1] = (int)end;
+    ++S.nsets;
+    lds = need > lds ? need : lds;
+    return 0;
+}
+
+int launch_sets(const char* who, bool bwd, int nsets, const UredAttnSet* sets, void* stream) {
+    URED_REQUIRE(nsets >= 1 && nsets <= URED_ATTN_MAX_SETS && sets, "%s: nsets=%d (1..%d)", who, nsets,
+                 URED_ATTN_MAX_SETS);
+    AttnSets S{};
+    size_t lds = 0;
+    for (int i = 0; i < nsets; ++i)
+        if (int rc = add_set(who, bwd, sets[i], S, lds)) return rc;
+    const int blocks = S.first[S.nsets];
+    if (blocks == 0) return 0;
+    if (bwd) hipLaunchKernelGGL(attn_bwd_kernel, dim3(blocks), dim3(ATT_THREADS), lds, (hipStream_t)stream, S);
+    else hipLaunchKernelGGL(attn_fwd_kernel, dim3(blocks), dim3(ATT_THREADS), lds, (hipStream_t)stream, S);
+    return ured::launch_status(who);
+}
+
 }  // namespace
 
 extern "C" {
@@ -174,31 +239,28 @@ int ured_attn_fwd(const float* q, int ldq, const float* k, int ldk, const float*
                   int B, int H, int n, int m, int d, float scale, float* out, int ldo, float* weights,
                   void* stream) {
     ured::clear_error();
-    if (int rc = check_sizes("ured_attn_fwd", B, H, n, m, d)) return rc;
-    URED_REQUIRE(fwd_lds(n, m, d) <= 65536, "ured_attn_fwd: n=%d m=%d d=%d needs more than 64 KB of LDS", n, m, d);
-    if (B == 0) return 0;
-    URED_REQUIRE(q && k && v && out && weights, "ured_attn_fwd: null pointer");
-    URED_REQUIRE(ldq >= H * d && ldk >= H * d && ldv >= H * d && ldo >= H * d, "ured_attn_fwd: row stride < H*d");
-    AttnArgs a{q, ldq, k, ldk, v, ldv, n, m, d, H, scale, out, ldo, weights, nullptr, 0, nullptr, 0, nullptr, 0,
-               nullptr, 0};
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3(B * H), dim3(ATT_THREADS), fwd_lds(n, m, d), (hipStream_t)stream, a);
-    return ured::launch_status("ured_attn_fwd");
+    const UredAttnSet x{q, ldq, k, ldk, v, ldv, B, H, n, m, d, scale, out, ldo, weights, nullptr, 0,
+                        nullptr, 0, nullptr, 0, nullptr, 0};
+    return launch_sets("ured_attn_fwd", false, 1, &x, stream);
 }
 
 int ured_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv, const float* weights,
                   const float* dout, int lddo, int B, int H, int n, int m, int d, float scale,
                   float* dq, int lddq, float* dk, int lddk, float* dv, int lddv, void* stream) {
     ured::clear_error();
-    if (int rc = check_sizes("ured_attn_bwd", B, H, n, m, d)) return rc;
-    URED_REQUIRE(bwd_lds(n, m, d) <= 65536, "ured_attn_bwd: n=%d m=%d d=%d needs more than 64 KB of LDS", n, m, d);
-    if (B == 0) return 0;
-    URED_REQUIRE(q && k && v && weights && dout && dq && dk && dv, "ured_attn_bwd: null pointer");
-    URED_REQUIRE(ldq >= H * d && ldk >= H * d && ldv >= H * d && lddo >= H * d && lddq >= H * d && lddk >= H * d &&
-                 lddv >= H * d, "ured_attn_bwd: row stride < H*d");
-    AttnArgs a{q, ldq, k, ldk, v, ldv, n, m, d, H, scale, nullptr, 0, const_cast<float*>(weights), dout, lddo,
-               dq, lddq, dk, lddk, dv, lddv};
-    hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * H), dim3(ATT_THREADS), bwd_lds(n, m, d), (hipStream_t)stream, a);
-    return ured::launch_status("ured_attn_bwd");
+    const UredAttnSet x{q, ldq, k, ldk, v, ldv, B, H, n, m, d, scale, nullptr, 0, const_cast<float*>(weights),
+                        dout, lddo, dq, lddq, dk, lddk, dv, lddv};
+    return launch_sets("ured_attn_bwd", true, 1, &x, stream);
+}
+
+int ured_attn_fwd_sets(int nsets, const UredAttnSet* sets, void* stream) {
+    ured::clear_error();
+    return launch_sets("ured_attn_fwd_sets", false, nsets, sets, stream);
+}
+
+int ured_attn_bwd_sets(int nsets, const UredAttnSet* sets, void* stream) {
+    ured::clear_error();
+    return launch_sets("ured_attn_bwd_sets", true, nsets, sets, stream);
 }
 
 }  // extern "C"

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libured_hip.so"
 # URED_LIB: an alternative build of the same ABI (A/B kernel experiments, tools/)
 LIB_PATH = os.environ.get("URED_LIB") or os.path.join(_HERE, LIB_NAME)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

@@ -40,7 +40,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 8   /* 8: ured_nn_bwd_set; 7: ured_copy_batch; 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
+#define URED_ABI_VERSION 9   /* 9: ured_attn_fwd_sets / ured_attn_bwd_sets; 8: ured_nn_bwd_set; 7: ured_copy_batch; 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
@@ -347,6 +347,27 @@ int ured_attn_fwd(const float* q, int ldq, const float* k, int ldk, const float*
 int ured_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv, const float* weights,
                   const float* dout, int lddo, int B, int H, int n, int m, int d, float scale,
                   float* dq, int lddq, float* dk, int lddk, float* dv, int lddv, void* stream);
+
+/* Up to URED_ATTN_MAX_SETS independent attention calls (e.g. the two node sets of one
+ * DescriptorsSelfAttention layer, attention_gnn.py:120-127: desc0 and desc1 through the same module)
+ * in ONE launch; each set is exactly the call above with its own fields (fwd: out / ldo / weights,
+ * bwd: weights / dout / dq / dk / dv), so the results are those of separate calls, bitwise. */
+#define URED_ATTN_MAX_SETS 2
+typedef struct {
+    const float* q; int ldq;
+    const float* k; int ldk;
+    const float* v; int ldv;
+    int B, H, n, m, d;
+    float scale;
+    float* out; int ldo;            /* forward output */
+    float* weights;                 /* [B*H*n*m]: written by the forward, read by the backward */
+    const float* dout; int lddo;    /* backward only */
+    float* dq; int lddq;
+    float* dk; int lddk;
+    float* dv; int lddv;
+} UredAttnSet;
+int ured_attn_fwd_sets(int nsets, const UredAttnSet* sets, void* stream);
+int ured_attn_bwd_sets(int nsets, const UredAttnSet* sets, void* stream);
 
 /* ---------------- graph-node layers (DeformNet_MatchingNet, node.hip) ----------------
  * Replace the node-level Conv1d(k=1) layers (in_proj_q/k/v, out_proj, the FeedForwardNet_norm

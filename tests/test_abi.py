@@ -32,6 +32,9 @@ def test_invalid_args_report_error_without_gpu(built):
         _lib.call("ured_nn_fwd", None, None, -1, 4, 4, 3, None, None, None, None, None)
     with pytest.raises(_lib.UredError, match="dirs"):
         _lib.call("ured_nn_seg_fwd", None, None, None, 1, 4, 4, 9, None, None, None, None, None)
+    import ured_hip.attn  # noqa: F401  (binds the attention entry points)
+    with pytest.raises(_lib.UredError, match="nsets"):
+        _lib.call("ured_attn_fwd_sets", 3, None, None)
 
 
 def test_library_is_gfx950(built):

@@ -66,6 +66,27 @@ def test_self_attention_matches_reference(dev, B, H, n, d):
     _close(x.grad, xr.grad)
 
 
+@pytest.mark.parametrize("B,H,n0,n1,d", [(16, 4, 2, 16, 128), (3, 2, 5, 7, 16), (2, 4, 32, 1, 8)])
+def test_self_attention_pair_equals_two_calls(dev, B, H, n0, n1, d):
+    """ured_attn_{fwd,bwd}_sets with the two node sets of a self-attention layer in one launch ==
+    two single-set calls, bitwise (output and the fused q|k|v gradient)."""
+    from ured_hip.attn import self_attention, self_attention_pair
+    g = torch.Generator().manual_seed(n0 * 7 + n1)
+    C = H * d
+    R0, R1 = B * n0, B * n1
+    qkv = torch.randn(R0 + R1, 3 * C, generator=g).to(dev)
+    go = torch.randn(R0 + R1, C, generator=g).to(dev)
+    x = qkv.clone().requires_grad_(True)
+    out = self_attention_pair(x, B, n0, n1, H)
+    out.backward(go)
+    x0 = qkv[:R0].clone().view(B, n0, 3 * C).requires_grad_(True)
+    x1 = qkv[R0:].clone().view(B, n1, 3 * C).requires_grad_(True)
+    o0, o1 = self_attention(x0, H), self_attention(x1, H)
+    torch.autograd.backward([o0, o1], [go[:R0].view(B, n0, C), go[R0:].view(B, n1, C)])
+    assert torch.equal(out[:R0], o0.reshape(R0, C)) and torch.equal(out[R0:], o1.reshape(R1, C))
+    assert torch.equal(x.grad[:R0], x0.grad.reshape(R0, 3 * C)) and torch.equal(x.grad[R0:], x1.grad.reshape(R1, 3 * C))
+
+
 def test_attention_rejects_oversize(dev):
     from ured_hip import _lib
     from ured_hip.attn import cross_attention
