@@ -23,6 +23,7 @@ from .attention import softmax_attention
 from .attention_utils import FeedForwardNet_norm, conv1x1
 
 _ATTN_PAIR = os.environ.get("URED_ATTN_PAIR", "1") == "1"     # A/B knob (tools/gpu_py_ab.sh)
+_NODE_ALIAS = os.environ.get("URED_NODE_ALIAS", "1") == "1"   # A/B knob (tools/gpu_py_ab.sh)
 
 
 class MultiheadAttention(nn.Module):
@@ -54,23 +55,31 @@ class MultiheadAttention(nn.Module):
     def _w(conv):
         return conv.weight.view(conv.weight.shape[0], -1)
 
-    def forward_nodes(self, xq, xkv=None):
+    def forward_nodes(self, xq, xkv=None, alias=False):
         """Node-major [B, n, C] query nodes and [B, m, C] key/value nodes (None: self-attention)
-        -> message [B, n, C]."""
+        -> message [B, n, C]. alias=True: (message, xq', xkv') where xq' [B*n, C] / xkv' [B*m, C]
+        (None for self-attention) are the projection's alias outputs of its inputs (NodeProjFn):
+        further consumers read those, and their gradients are added inside the projection's
+        backward instead of by autograd."""
         if self.attention_func is not softmax_attention:
             raise NotImplementedError("node-major path implements the softmax attention only")
         q_, k_, v_ = self.in_proj_q, self.in_proj_k, self.in_proj_v
         B, n, C = xq.shape
+        xq_a = xkv_a = None
         if xkv is None:
-            qkv = node_proj((xq.reshape(B * n, C),), [(self._w(q_), self._w(k_), self._w(v_))],
-                            [(q_.bias, k_.bias, v_.bias)])
+            r = node_proj((xq.reshape(B * n, C),), [(self._w(q_), self._w(k_), self._w(v_))],
+                          [(q_.bias, k_.bias, v_.bias)], aliases=(alias,))
+            qkv, xq_a = r if alias else (r, None)
             out = self_attention(qkv.view(B, n, 3 * C), self.num_heads)
         else:
             m = xkv.shape[1]
-            q, kv = node_proj((xq.reshape(B * n, C), xkv.reshape(B * m, C)),
-                              [(self._w(q_),), (self._w(k_), self._w(v_))], [(q_.bias,), (k_.bias, v_.bias)])
+            r = node_proj((xq.reshape(B * n, C), xkv.reshape(B * m, C)),
+                          [(self._w(q_),), (self._w(k_), self._w(v_))], [(q_.bias,), (k_.bias, v_.bias)],
+                          aliases=(alias, alias))
+            q, kv, xq_a, xkv_a = r if alias else (*r, None, None)
             out = cross_attention(q.view(B, n, C), kv.view(B, m, 2 * C), self.num_heads)
-        return node_linear(out.reshape(B * n, C), self._w(self.out_proj), self.out_proj.bias).view(B, n, C)
+        msg = node_linear(out.reshape(B * n, C), self._w(self.out_proj), self.out_proj.bias).view(B, n, C)
+        return (msg, xq_a, xkv_a) if alias else msg
 
 
 class ResidualAttentionMessagePropagation(nn.Module):
@@ -86,15 +95,26 @@ class ResidualAttentionMessagePropagation(nn.Module):
         return desc_q + self.fc(torch.cat([first, message], dim=1))
 
     def forward_nodes(self, xq, xkv=None):
+        return self.forward_nodes_alias(xq, xkv)[0]
+
+    def forward_nodes_alias(self, xq, xkv=None):
+        """(forward_nodes(xq, xkv), xkv') where xkv' [B, m, C] (None without xkv) stands for xkv
+        in any later use: the projection returns its inputs as alias outputs (NodeProjFn), so the
+        gradients of a node tensor's several consumers (q / k|v projection, the FFN, the next call)
+        are summed inside the projection backward's epilogue, not by autograd adds."""
         if not self._node_ffn_ok():
             message = self.mha.forward_nodes(xq, xkv)
             first = xq - message if self.use_offset else xq
-            return xq + self.fc.forward_nodes(torch.cat([first, message], dim=-1))
-        message = self.mha.forward_nodes(xq, xkv)
+            return xq + self.fc.forward_nodes(torch.cat([first, message], dim=-1)), xkv
         B, n, C = xq.shape
-        x2, m2 = xq.reshape(B * n, C), message.reshape(B * n, C)
+        if _NODE_ALIAS:
+            message, x2, xkv_a = self.mha.forward_nodes(xq, xkv, alias=True)
+            xkv_a = None if xkv_a is None else xkv_a.view(xkv.shape)
+        else:
+            message, x2, xkv_a = self.mha.forward_nodes(xq, xkv), xq.reshape(B * n, C), xkv
+        m2 = message.reshape(B * n, C)
         first, R = (x2 - m2, x2) if self.use_offset else (x2, None)
-        return node_ffn(self.fc, first, m2, R, (0, B * n)).view(B, n, C)
+        return node_ffn(self.fc, first, m2, R, (0, B * n)).view(B, n, C), xkv_a
 
     def _node_ffn_ok(self):
         return self.fc.use_norm == "use_bn" and len(self.fc) == 4
@@ -114,7 +134,11 @@ class ResidualAttentionMessagePropagation(nn.Module):
         R0, R1 = B * n0, B * n1
         X = torch.cat([x0.reshape(R0, C), x1.reshape(R1, C)])
         q_, k_, v_ = mha.in_proj_q, mha.in_proj_k, mha.in_proj_v
-        qkv = node_proj((X,), [(mha._w(q_), mha._w(k_), mha._w(v_))], [(q_.bias, k_.bias, v_.bias)])
+        # X's second consumer (the FFN) reads the projection's alias of it (NodeProjFn)
+        qkv = node_proj((X,), [(mha._w(q_), mha._w(k_), mha._w(v_))], [(q_.bias, k_.bias, v_.bias)],
+                        aliases=(_NODE_ALIAS,))
+        if _NODE_ALIAS:
+            qkv, X = qkv
         if _ATTN_PAIR:
             # both sets' attention in one launch each way, reading / writing row blocks of qkv / o
             o = self_attention_pair(qkv, B, n0, n1, mha.num_heads)
@@ -150,8 +174,11 @@ class DescriptorsCrossAttention(nn.Module):
         return desc0, self.module(desc1, desc0)
 
     def forward_nodes(self, desc0, desc1):
-        desc0 = self.module.forward_nodes(desc0, desc1)     # the updated desc0 feeds desc1's update
-        return desc0, self.module.forward_nodes(desc1, desc0)
+        # the updated desc0 feeds desc1's update; each call hands back its key/value input as an
+        # alias for the next use (see ResidualAttentionMessagePropagation.forward_nodes_alias)
+        desc0, desc1 = self.module.forward_nodes_alias(desc0, desc1)
+        desc1, desc0 = self.module.forward_nodes_alias(desc1, desc0)
+        return desc0, desc1
 
 
 class GraphAttentionNet(nn.Module):

@@ -364,10 +364,14 @@ class NodeProjFn(Function):
     gradients are written (or, for a second use of the layer, accumulated) straight into the flat
     gradient. All GEMMs of one direction run in one launch.
 
-    apply(groups, x_0, .., x_{n-1}, then per input: its weights, then its biases)."""
+    apply(groups, aliases, x_0, .., x_{n-1}, then per input: its weights, then its biases).
+    aliases[i]: also return x_i itself (after the projections) for a second consumer of the node
+    features (DeformNet's FFN reads the query nodes, the next call the key / value nodes); its
+    gradient then arrives in this backward and is added inside the dgrad's epilogue (R) instead of
+    in a separate autograd add (the pattern of ops.PartRowsFn's alias output)."""
 
     @staticmethod
-    def forward(ctx, groups, *tensors):
+    def forward(ctx, groups, aliases, *tensors):
         n = len(groups)
         xs, rest = tensors[:n], tensors[n:]
         _lib.require_device(*xs)
@@ -383,16 +387,22 @@ class NodeProjFn(Function):
             jobs.append(linear_desc(x, Wf, y, bias=bf))
             ys.append(y)
         launch(*jobs)
-        ctx.groups = groups
+        ctx.groups, ctx.aliases = groups, aliases
         ctx.save_for_backward(*xs, *rest)
-        return tuple(ys) if n > 1 else ys[0]
+        outs = tuple(ys) + tuple(x for x, a in zip(xs, aliases) if a)
+        return outs if len(outs) > 1 else outs[0]
 
     @staticmethod
     def backward(ctx, *gs):
-        groups = ctx.groups
+        groups, aliases = ctx.groups, ctx.aliases
         n = len(groups)
         saved = ctx.saved_tensors
         xs, rest = saved[:n], saved[n:]
+        galias, q = [None] * n, n
+        for i, a in enumerate(aliases):
+            if a:
+                galias[i] = gs[q]
+                q += 1
         jobs, dxs, fins, o = [], [], [], 0
         for i, gsz in enumerate(groups):
             w, b = rest[o:o + gsz], rest[o + gsz:o + 2 * gsz]
@@ -400,26 +410,28 @@ class NodeProjFn(Function):
             g = _rows(gs[i])
             x = xs[i]
             dx = torch.empty(x.shape, device=x.device)
+            R = None if galias[i] is None else _rows(galias[i])
             dW, aW, fW = _grad_rows(w)
             db, ab, fb = _grad_rows(b)
-            jobs += [dgrad_desc(g, _stack_rows(w), dx), wgrad_desc(g, x, dW, accumulate=aW),
+            jobs += [dgrad_desc(g, _stack_rows(w), dx, R=R), wgrad_desc(g, x, dW, accumulate=aW),
                      colsum_desc(g, db, accumulate=ab)]
             dxs.append(dx)
             fins.append((fW, fb))
         launch(*jobs)
-        out = [None] + dxs
+        out = [None, None] + dxs
         for fW, fb in fins:
             out += fW() + fb()
         return tuple(out)
 
 
-def node_proj(xs, groups_w, groups_b):
+def node_proj(xs, groups_w, groups_b, aliases=None):
     """NodeProjFn over inputs xs with weight groups groups_w[i] (tuples of [N_j, K] tensors) and
-    bias groups groups_b[i]."""
+    bias groups groups_b[i]; aliases[i] (optional): also return xs[i] (see NodeProjFn)."""
     args = list(xs)
     for w, b in zip(groups_w, groups_b):
         args += list(w) + list(b)
-    return NodeProjFn.apply(tuple(len(w) for w in groups_w), *args)
+    aliases = tuple(bool(a) for a in aliases) if aliases is not None else (False,) * len(xs)
+    return NodeProjFn.apply(tuple(len(w) for w in groups_w), aliases, *args)
 
 
 class NodeFFNFn(Function):
