@@ -844,6 +844,69 @@ __global__ __launch_bounds__(256) void get_shape_bwd_kernel(const float* __restr
     if (t < 6) gp[6 * (size_t)bp + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
 }
 
+// get_shape straight from the source database (the training step's form): part slot j reads
+// mats[src_j] with src_j = labels[j] (+ nsrc when negative: python indexing,
+// dataset_utils.py:800-805) instead of a gathered [nparts, rows, 6] copy, and builds its six
+// parameters as weight * param + default in-kernel (the mul and the add of get_shape, in that
+// order, rounded separately: bitwise the composed form). The backward returns
+// weight * sum_r A grad_out (MulBackward's product after the same fixed-order reduction).
+__device__ __forceinline__ long long src_row(const long long* labels, int nsrc, long long j) {
+    long long s = labels[j];
+    s = s < 0 ? s + nsrc : s;
+    URED_DBG_CHECK(s >= 0 && s < nsrc);
+    return s < 0 ? 0 : (s >= nsrc ? nsrc - 1 : s);   // out-of-range labels read a valid row
+}
+
+__global__ __launch_bounds__(256) void get_shape_src_fwd_kernel(const float* __restrict__ mats,
+        const long long* __restrict__ labels, int nsrc, const float* __restrict__ param,
+        const float* __restrict__ dflt, float weight, int R, long long total, float* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;
+    const long long bp = i / R, r = i - bp * R;
+    const float2* a = reinterpret_cast<const float2*>(mats + 6 * (src_row(labels, nsrc, bp) * R + r));
+    float pp[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const float w = weight * param[6 * bp + k];
+        pp[k] = dflt ? w + dflt[6 * bp + k] : w;
+    }
+    const float2 a0 = a[0], a1 = a[1], a2 = a[2];
+    float v = a0.x * pp[0];
+    v = __builtin_fmaf(a0.y, pp[1], v);
+    v = __builtin_fmaf(a1.x, pp[2], v);
+    v = __builtin_fmaf(a1.y, pp[3], v);
+    v = __builtin_fmaf(a2.x, pp[4], v);
+    v = __builtin_fmaf(a2.y, pp[5], v);
+    out[i] = v;
+}
+
+__global__ __launch_bounds__(256) void get_shape_src_bwd_kernel(const float* __restrict__ mats,
+        const long long* __restrict__ labels, int nsrc, const float* __restrict__ g, float weight, int R,
+        float* __restrict__ gparam) {
+    __shared__ float red[4][6];
+    const int bp = blockIdx.x, t = threadIdx.x;
+    const float* a = mats + (size_t)src_row(labels, nsrc, bp) * R * 6;
+    const float* gg = g + (size_t)bp * R;
+    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = t; r < R; r += 256) {
+        const float2* ar = reinterpret_cast<const float2*>(a + 6 * (size_t)r);
+        const float2 a0 = ar[0], a1 = ar[1], a2 = ar[2];
+        const float gv = gg[r];
+        acc[0] = __builtin_fmaf(a0.x, gv, acc[0]); acc[1] = __builtin_fmaf(a0.y, gv, acc[1]);
+        acc[2] = __builtin_fmaf(a1.x, gv, acc[2]); acc[3] = __builtin_fmaf(a1.y, gv, acc[3]);
+        acc[4] = __builtin_fmaf(a2.x, gv, acc[4]); acc[5] = __builtin_fmaf(a2.y, gv, acc[5]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) acc[k] += __shfl_xor(acc[k], o);
+    if ((t & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[t >> 6][k] = acc[k];
+    __syncthreads();
+    if (t < 6) gparam[6 * (size_t)bp + t] = weight * ((red[0][t] + red[1][t]) + (red[2][t] + red[3][t]));
+}
+
 }  // namespace
 
 extern "C" {
@@ -987,6 +1050,33 @@ int ured_get_shape_bwd(const float* A, const float* grad_out, int nparts, int ro
     URED_REQUIRE(((uintptr_t)A & 7) == 0, "ured_get_shape_bwd: A must be 8-byte aligned");
     hipLaunchKernelGGL(get_shape_bwd_kernel, dim3(nparts), dim3(256), 0, (hipStream_t)stream, A, grad_out, rows, grad_p);
     return ured::launch_status("ured_get_shape_bwd");
+}
+
+int ured_get_shape_src_fwd(const float* mats, const long long* labels, int nsrc, const float* param,
+                           const float* dflt, float weight, int nparts, int rows, float* out, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(nparts >= 0 && rows >= 0 && nsrc >= 0, "ured_get_shape_src_fwd: negative size");
+    if (nparts == 0 || rows == 0) return 0;
+    URED_REQUIRE(nsrc > 0, "ured_get_shape_src_fwd: empty source database");
+    URED_REQUIRE(mats && labels && param && out, "ured_get_shape_src_fwd: null pointer");
+    URED_REQUIRE(((uintptr_t)mats & 7) == 0, "ured_get_shape_src_fwd: mats must be 8-byte aligned");
+    const long long total = (long long)nparts * rows;
+    hipLaunchKernelGGL(get_shape_src_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, mats, labels, nsrc, param, dflt, weight, rows, total, out);
+    return ured::launch_status("ured_get_shape_src_fwd");
+}
+
+int ured_get_shape_src_bwd(const float* mats, const long long* labels, int nsrc, const float* grad_out, float weight,
+                           int nparts, int rows, float* grad_param, void* stream) {
+    ured::clear_error();
+    URED_REQUIRE(nparts >= 0 && rows >= 0 && nsrc >= 0, "ured_get_shape_src_bwd: negative size");
+    if (nparts == 0) return 0;
+    URED_REQUIRE(nsrc > 0, "ured_get_shape_src_bwd: empty source database");
+    URED_REQUIRE(mats && labels && grad_out && grad_param, "ured_get_shape_src_bwd: null pointer");
+    URED_REQUIRE(((uintptr_t)mats & 7) == 0, "ured_get_shape_src_bwd: mats must be 8-byte aligned");
+    hipLaunchKernelGGL(get_shape_src_bwd_kernel, dim3(nparts), dim3(256), 0, (hipStream_t)stream, mats, labels, nsrc,
+                       grad_out, weight, rows, grad_param);
+    return ured::launch_status("ured_get_shape_src_bwd");
 }
 
 int ured_seg_aabb(const float* x, const int* off, int G, float* out, void* stream) {

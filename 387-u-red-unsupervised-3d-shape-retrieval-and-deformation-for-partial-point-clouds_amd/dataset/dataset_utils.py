@@ -40,6 +40,21 @@ def get_shape(A, param, src_default_param=None, weight=1.0, param_init=None, con
     return torch.bmm(A, p).reshape(bs, num_part, -1, 3)
 
 
+def get_shape_src(db, source_labels, param, src_default_param=None, weight=1.0):
+    """get_shape(get_source_info(source_labels, db)[0], param, src_default_param, weight) — the
+    training step's deformation (engine/train.py:222-223) — reading the source matrices in place:
+    one HIP launch each way (ured_hip.ops.GetShapeSrcFn), no gathered [B, P, 3n, 6] copy and no
+    separate parameter mul / add. Same values, bitwise."""
+    bs, num_part, pd = param.shape
+    if pd == 6 and param.is_cuda and not db.mats.requires_grad:
+        from ured_hip.ops import GetShapeSrcFn
+        labels = torch.as_tensor(source_labels, device=db.mats.device).long()
+        out = GetShapeSrcFn.apply(db.mats.reshape(db.mats.shape[0], -1, pd), labels, param, src_default_param, weight)
+        return out.reshape(bs, num_part, -1, 3)
+    mats = get_source_info(source_labels, db, want=(True, False, False))[0]
+    return get_shape(mats, param, src_default_param, weight)
+
+
 _MIRROR = {}
 
 

@@ -39,7 +39,8 @@ if os.path.dirname(_HERE) not in sys.path:
 
 from dataset import synthetic  # noqa: E402
 from engine.config import check_config  # noqa: E402
-from dataset.dataset_utils import get_shape, get_source_info, get_source_points, get_symmetric  # noqa: E402
+from dataset.dataset_utils import (get_shape, get_shape_src, get_source_info, get_source_points,  # noqa: E402
+                                   get_symmetric)
 from loss.basic_consistency_loss import compute_pc_consistency, compute_pc_consistency_weighted  # noqa: E402
 from loss.basic_loss import residual_retrieval_loss  # noqa: E402
 from loss.chamfer_loss import compute_cm_loss, compute_cm_loss_pair  # noqa: E402
@@ -52,6 +53,8 @@ from train_utils.load_sources import load_sources  # noqa: E402
 from train_utils.optimizer_dm import define_optimizer_dm_re_recon  # noqa: E402
 from ured_hip.kernels import RowWeights  # noqa: E402
 from ured_hip.ops import PartBounds, UniqueRows, build_parts, part_aabb, part_rows, upload  # noqa: E402
+
+_SHAPE_SRC = os.environ.get("URED_SHAPE_SRC", "1") == "1"     # A/B knob (tools/gpu_py_ab.sh)
 
 MODULE_NAMES = ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "re_residual_net_full",
                 "src_encoder_all", "recon_decoder_src", "embedding_layer")
@@ -233,8 +236,9 @@ class TrainStep:
         B, N, _ = x.shape
         src_labels = batch["src_labels"]
         uq = batch.get("src_unique") if cfg.get("unique_sources", True) else None
-        # the unique-source path embeds the distinct parts' semantics itself (_source_branch)
-        mats, _, src_sem_idx = get_source_info(src_labels, self.db, want=(True, False, uq is None))
+        # the unique-source path embeds the distinct parts' semantics itself (_source_branch); the
+        # source matrices are read in place by get_shape_src
+        mats, _, src_sem_idx = get_source_info(src_labels, self.db, want=(not _SHAPE_SRC, False, uq is None))
         emb = M["embedding_layer"]
         with torch.no_grad():          # the embedding is not trained (optimizer_dm.py:83)
             src_sem_f = emb(src_sem_idx) if uq is None else None
@@ -250,7 +254,8 @@ class TrainStep:
                                                                                  batch["labels"], x, alias=True)
         codes = codes.view(B, P, -1)
         params_full = M["param_decoder_full"](tcode, codes, None)
-        out = get_shape(mats, params_full, param_def, cfg["alpha"]).reshape(B, -1, 3)
+        out = (get_shape_src(self.db, src_labels, params_full, param_def, cfg["alpha"]) if _SHAPE_SRC else
+               get_shape(mats, params_full, param_def, cfg["alpha"])).reshape(B, -1, 3)
         recon_full_p = M["recon_decoder_full"].forward_split(pp_alias.view(B * N, -1), tcode,
                                                              group_rows=N).view(B, N, 3)
         re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,

@@ -33,6 +33,8 @@ _SIGNATURES = {
     "ured_part_rows_bwd_add": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
     "ured_get_shape_fwd": [_P, _P, _I, _I, _P, _P],
     "ured_get_shape_bwd": [_P, _P, _I, _I, _P, _P],
+    "ured_get_shape_src_fwd": [_P, _P, _I, _P, _P, ctypes.c_float, _I, _I, _P, _P],
+    "ured_get_shape_src_bwd": [_P, _P, _I, _P, ctypes.c_float, _I, _I, _P, _P],
     "ured_emd_workspace": [_I, _I],
     "ured_emd_fwd": [_P, _P, _I, _I, _F, _I, _P, _P, _P, _SZ, _P],
     "ured_emd_bwd": [_P, _P, _I, _I, _P, _P, _P, _P],

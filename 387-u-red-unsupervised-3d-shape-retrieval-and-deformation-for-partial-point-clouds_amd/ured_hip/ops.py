@@ -58,6 +58,42 @@ class GetShapeFn(Function):
         return None, gp
 
 
+class GetShapeSrcFn(Function):
+    """get_shape(get_source_info(labels)[0], param, dflt, weight) without the gathered copy of the
+    source matrices and without the mul / add / MulBackward kernels (ured_get_shape_src_fwd/bwd):
+    out [J, R] with part slot j reading mats[labels[j]] (python negative indexing); gradient for
+    param only (the matrices are data, dflt the parts' boxes). Bitwise the composed form."""
+
+    @staticmethod
+    def forward(ctx, mats, labels, param, dflt, weight):
+        if mats.requires_grad or (dflt is not None and dflt.requires_grad):
+            raise NotImplementedError("get_shape_src: gradients w.r.t. the source matrices / defaults")
+        _lib.require_device(mats, labels, param)
+        if mats.dtype != torch.float32 or not mats.is_contiguous() or labels.dtype != torch.int64:
+            raise TypeError("get_shape_src: mats must be contiguous float32 [S, R, 6], labels int64")
+        S, R, pd = mats.shape
+        J = labels.numel()
+        p = param.contiguous().float().reshape(J, pd)
+        d = None if dflt is None else dflt.contiguous().float().reshape(J, pd)
+        lab = labels.contiguous().reshape(J)
+        out = torch.empty(J, R, device=mats.device, dtype=torch.float32)
+        _lib.call("ured_get_shape_src_fwd", _lib.ptr(mats), _lib.ptr(lab), S, _lib.ptr(p), _lib.ptr(d), float(weight),
+                  J, R, _lib.ptr(out), _lib.stream_of(mats))
+        ctx.save_for_backward(mats, lab)
+        ctx.weight, ctx.pshape = float(weight), param.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        mats, lab = ctx.saved_tensors
+        S, R, _ = mats.shape
+        J = lab.numel()
+        gp = torch.empty(J, 6, device=mats.device, dtype=torch.float32)
+        _lib.call("ured_get_shape_src_bwd", _lib.ptr(mats), _lib.ptr(lab), S, _lib.ptr(g.contiguous()), ctx.weight,
+                  J, R, _lib.ptr(gp), _lib.stream_of(mats))
+        return None, None, gp.view(ctx.pshape), None, None
+
+
 class PermuteRowsFn(Function):
     """out[b, i] = x[b, perm[b, i]] for a per-sample permutation perm [B, N]; the backward is the
     gather by the inverse permutation (torch.gather's backward would scatter_add into zeros)."""

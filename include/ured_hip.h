@@ -40,7 +40,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 9   /* 9: ured_attn_fwd_sets / ured_attn_bwd_sets; 8: ured_nn_bwd_set; 7: ured_copy_batch; 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
+#define URED_ABI_VERSION 9   /* 9: ured_attn_fwd_sets / ured_attn_bwd_sets, ured_get_shape_src_fwd / _bwd; 8: ured_nn_bwd_set; 7: ured_copy_batch; 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
@@ -103,6 +103,15 @@ int ured_nn_seg_fwd_ws(const float* a, const float* b, const int* segs, int nseg
  * default); the backward gives grad_p[j, k] = sum_r A[j, r, k] grad_out[j, r] (deterministic). */
 int ured_get_shape_fwd(const float* A, const float* p, int nparts, int rows, float* out, void* stream);
 int ured_get_shape_bwd(const float* A, const float* grad_out, int nparts, int rows, float* grad_p, void* stream);
+/* The training step's form (engine/train.py:222-223: get_source_info + get_shape): part slot j reads
+ * mats + src_j * rows * 6, src_j = labels[j] (int64; + nsrc when negative, python indexing), so no
+ * gathered copy of the source matrices; p[j] = weight * param[j] + dflt[j] (dflt may be NULL) is
+ * formed in-kernel with get_shape's separate mul and add; the backward writes
+ * grad_param = weight * sum_r A grad_out. */
+int ured_get_shape_src_fwd(const float* mats, const long long* labels, int nsrc, const float* param,
+                           const float* dflt, float weight, int nparts, int rows, float* out, void* stream);
+int ured_get_shape_src_bwd(const float* mats, const long long* labels, int nsrc, const float* grad_out, float weight,
+                           int nparts, int rows, float* grad_param, void* stream);
 
 /* Per-part axis-aligned boxes (compute_aabbox, dataset/dataset_utils.py:77-85, as used by
  * get_part, engine/train.py:119-128): x [R,3] points sorted by segment, off int32 [G+1] row

@@ -61,6 +61,33 @@ def test_get_shape_hip_matches_bmm(dev):
     assert torch.equal(prm.grad, g1)
 
 
+@pytest.mark.parametrize("with_dflt", [True, False])
+def test_get_shape_src_equals_gathered(dev, with_dflt):
+    """The training step's get_shape_src (matrices read in place by source label, the parameter
+    mul / add in-kernel) == get_shape over the gathered matrices, bitwise, values and gradient;
+    negative labels index from the end (python indexing, dataset_utils.py:800-805)."""
+    from dataset.dataset_utils import get_shape, get_shape_src, get_source_info
+    from train_utils.load_sources import SourceDB
+    g = torch.Generator().manual_seed(3)
+    S, n, B, P = 40, 512, 4, 16
+    mats = torch.randn(S, 3 * n, 6, generator=g)
+    db = SourceDB(torch.randn(S, n, 3, generator=g), mats, torch.randn(S, 6, generator=g),
+                  torch.randint(0, 4, (S,), generator=g), dev)
+    labels = torch.randint(-S, S, (B, P), generator=g).to(dev)
+    prm = torch.randn(B, P, 6, generator=g).to(dev)
+    dflt = torch.randn(B, P, 6, generator=g).to(dev) if with_dflt else None
+    go = torch.randn(B, P, n, 3, generator=g).to(dev)
+    a = prm.clone().requires_grad_(True)
+    out = get_shape_src(db, labels, a, dflt, 0.3)
+    out.backward(go)
+    b = prm.clone().requires_grad_(True)
+    A = get_source_info(labels, db, want=(True, False, False))[0]
+    ref = get_shape(A, b, dflt, 0.3)
+    ref.backward(go)
+    assert torch.equal(out, ref)
+    assert torch.equal(a.grad, b.grad)
+
+
 @pytest.mark.parametrize("B,N,P,C,kmax", [(16, 2048, 16, 512, 4), (3, 700, 16, 6, 16), (2, 5, 8, 3, 8)])
 def test_part_rows_matches_separate_ops(dev, B, N, P, C, kmax):
     """PartRowsFn (gather by part label + per-part sums, one-pass HIP backward) vs the separate
