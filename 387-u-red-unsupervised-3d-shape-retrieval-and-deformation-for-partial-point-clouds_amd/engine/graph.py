@@ -165,7 +165,7 @@ class GraphedStep:
             # issues (ranks can miss a graph at different steps: their collective sequences must
             # still match)
             self.inner.begin_backward()
-        loss.backward()
+        self.inner.backward_loss(loss)
         del loss
         self.inner.reduce_gradients()
         self.inner.clip_and_step()
@@ -192,7 +192,7 @@ class GraphedStep:
                 loss, T = self.inner.forward(static, epoch)
                 if reduced:
                     self.inner.begin_backward()      # bucket all-reduces from the hooks
-                loss.backward()
+                self.inner.backward_loss(loss)
                 if reduced:
                     self.inner.reduce_gradients()    # remaining buckets, waits, 1/world (flat views)
                 elif flat:

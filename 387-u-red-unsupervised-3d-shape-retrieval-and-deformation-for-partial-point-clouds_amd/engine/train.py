@@ -353,10 +353,18 @@ class TrainStep:
         self.optimizer.zero_grad(set_to_none=True)
         loss, T = self.forward(batch, epoch)
         self.begin_backward()
-        loss.backward()
+        self.backward_loss(loss)
         self.reduce_gradients()
         self.clip_and_step()
         return T
+
+    def backward_loss(self, loss):
+        """loss.backward() seeded with a persistent 1.0 (no fill kernel per step; a HIP-graph
+        capture reads the same tensor)."""
+        seed = getattr(self, "_seed", None)
+        if seed is None or seed.device != loss.device or seed.dtype != loss.dtype:
+            seed = self._seed = torch.ones((), device=loss.device, dtype=loss.dtype)
+        loss.backward(seed)
 
     def begin_backward(self):
         """Data-parallel hook before loss.backward() (engine/dp.py: arms the bucket all-reduce)."""
