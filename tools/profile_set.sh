@@ -8,4 +8,4 @@ bash tools/prof_step.sh $T 20 > gpurun_out/${T}_prof_step.log 2>&1 || { tail -20
 head -12 gpurun_out/${T}_trace_timed_top.txt
 bash tools/gpu_prof.sh $T > gpurun_out/${T}_gpu_prof.log 2>&1 || { tail -20 gpurun_out/${T}_gpu_prof.log; exit 1; }
 bash tools/gpu_clock_sq.sh $T > gpurun_out/${T}_clock_sq.log 2>&1 || { tail -20 gpurun_out/${T}_clock_sq.log; exit 1; }
-python3 -c "import json; d=json.load(open('gpurun_out/${T}_pmc_summary.json')); [print(k[:80], v.get('hbm_bytes_per_launch')) for k,v in d.items() if 'gemm2' in k]" | head -8
+python3 -c "import json; d=json.load(open('gpurun_out/${T}_pmc_summary.json')); [print(k[:80], v.get('hbm_bytes_per_launch')) for k,v in [x for x in d.items() if 'gemm2' in x[0]][:8]]"
