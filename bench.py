@@ -34,12 +34,12 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X fp32 (vector = matrix) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARY = "r6p_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
+PMC_SUMMARY = "r6s_pmc_summary.json"   # FETCH/WRITE_SIZE passes of this default command (tools/gpu_prof.sh)
 # rocprofv3 --kernel-trace --stats of the headline command (tools/prof_step.sh), restricted to its timed
 # steps: the dominant kernel's average duration there is what roofline.achieved / frac are computed from
-PROF_STATS = "r6p_step_kernel_stats.csv"
-CLOCK_SUMMARY = "r6p_clock_summary.json"   # GRBM_GUI_ACTIVE pass (tools/gpu_clock_sq.sh): clock held per kernel
-SQ_SUMMARY = "r6p_sq_summary.json"         # SQ pass (tools/gpu_clock_sq.sh): MFMA-busy cycles per kernel
+PROF_STATS = "r6s_step_kernel_stats.csv"
+CLOCK_SUMMARY = "r6s_clock_summary.json"   # GRBM_GUI_ACTIVE pass (tools/gpu_clock_sq.sh): clock held per kernel
+SQ_SUMMARY = "r6s_sq_summary.json"         # SQ pass (tools/gpu_clock_sq.sh): MFMA-busy cycles per kernel
 NOMINAL_GHZ = 2.4
 
 
