@@ -423,80 +423,38 @@ __device__ __forceinline__ float row_dot(const float* v, const float* row, int C
     return (d0 + d1) + (d2 + d3);
 }
 
-// R rows per workgroup (CT_ROWS when their LDS images fit): the other side's rows are read from
-// L2 once per R rows instead of once per row (the per-row form re-read all of s / t for every row:
-// 512 workgroups x 512 KB at config 2). Every dot product, sum and store is the per-row form's,
-// in the same order, so the results do not depend on R.
-#ifndef URED_CT_ROWS
-#define URED_CT_ROWS 4
-#endif
-constexpr int CT_ROWS = URED_CT_ROWS;
-
-// R dot products of one global row against R LDS rows: the row is read once (float4), each dot
-// keeps row_dot's four accumulators and combine order
-template <int R>
-__device__ __forceinline__ void row_dots(const float* v, int ldv, const float* row, int C, int nr, float (&out)[R]) {
-    const float4* r4 = reinterpret_cast<const float4*>(row);
-    float d[R][4];
-#pragma unroll
-    for (int r = 0; r < R; ++r) d[r][0] = d[r][1] = d[r][2] = d[r][3] = 0.f;
-    const int C4 = C >> 2;
-#pragma unroll 2
-    for (int q = 0; q < C4; ++q) {
-        const float4 x = r4[q];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (r >= nr) break;
-            const float4 y = reinterpret_cast<const float4*>(v + (size_t)r * ldv)[q];
-            d[r][0] += x.x * y.x; d[r][1] += x.y * y.y; d[r][2] += x.z * y.z; d[r][3] += x.w * y.w;
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) out[r] = (d[r][0] + d[r][1]) + (d[r][2] + d[r][3]);
-}
-
-// rows i0 .. i0+nr-1 of t into trow[R][C] (LDS) and their logits against every s row into lg[R][n_all]:
-// scale * (t_i . s_j) * inv_t * inv_s (thread j takes row j)
-template <int R>
-__device__ __forceinline__ void logits_rows(const ContrastArgs& a, int i0, int nr, float* trow, float* lg) {
-    for (int e = threadIdx.x; e < nr * a.C; e += LT) trow[e] = a.t[(size_t)i0 * a.C + e];
+// logits of t row i against every s row into lg[] (LDS): scale * (t_i . s_j) * inv_t * inv_s
+// (thread j takes row j: 256 rows in flight per workgroup)
+__device__ __forceinline__ void logits_row(const ContrastArgs& a, int i, float* trow, float* lg) {
+    for (int c = threadIdx.x; c < a.C; c += LT) trow[c] = a.t[(size_t)i * a.C + c];
     __syncthreads();
-    for (int j = threadIdx.x; j < a.n_all; j += LT) {
-        float dots[R];
-        row_dots<R>(trow, a.C, a.s + (size_t)j * a.C, a.C, nr, dots);
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (r < nr) lg[r * a.n_all + j] = dots[r] * (a.inv[i0 + r] * a.scale) * a.inv[a.n + j];
-    }
+    const float it = a.inv[i] * a.scale;
+    for (int j = threadIdx.x; j < a.n_all; j += LT)
+        lg[j] = row_dot(trow, a.s + (size_t)j * a.C, a.C) * it * a.inv[a.n + j];
     __syncthreads();
 }
 
-template <int R>
 __global__ __launch_bounds__(LT) void contrast_fwd_kernel(ContrastArgs a) {
-    extern __shared__ float lds[];           // [R][C] t rows, [R][n_all] logits
+    extern __shared__ float lds[];           // [C] t row, [n_all] logits
     __shared__ float shf[LT];
     __shared__ double shd[LT];
     float* trow = lds;
-    float* lg = lds + R * a.C;
-    const int i0 = blockIdx.x * R, nr = min(R, a.n - i0), t = threadIdx.x;
-    logits_rows<R>(a, i0, nr, trow, lg);
-    for (int r = 0; r < nr; ++r) {
-        const int i = i0 + r;
-        const float* l_ = lg + r * a.n_all;
-        float m = -__builtin_inff();
-        for (int j = t; j < a.n_all; j += LT) m = fmaxf(m, l_[j]);
-        m = block_max(m, shf);
-        float se = 0.f;
-        for (int j = t; j < a.n_all; j += LT) se += expf(l_[j] - m);
-        se = block_sum(se, shf);
-        const bool valid = a.src_labels[i] != -1;
-        URED_DBG_CHECK(!valid || (a.s_off + i >= 0 && a.s_off + i < a.n_all));   // the label's logit (LDS)
-        if (t == 0) {
-            const float l = m + logf(se);
-            a.lse[i] = l;
-            st_agent(a.part + 2 * i, valid ? l - l_[a.s_off + i] : 0.f);
-            st_agent(a.part + 2 * i + 1, valid ? 1.f : 0.f);
-        }
+    float* lg = lds + a.C;
+    const int i = blockIdx.x, t = threadIdx.x;
+    logits_row(a, i, trow, lg);
+    float m = -__builtin_inff();
+    for (int j = t; j < a.n_all; j += LT) m = fmaxf(m, lg[j]);
+    m = block_max(m, shf);
+    float se = 0.f;
+    for (int j = t; j < a.n_all; j += LT) se += expf(lg[j] - m);
+    se = block_sum(se, shf);
+    const bool valid = a.src_labels[i] != -1;
+    URED_DBG_CHECK(!valid || (a.s_off + i >= 0 && a.s_off + i < a.n_all));   // the label's logit (LDS)
+    if (t == 0) {
+        const float l = m + logf(se);
+        a.lse[i] = l;
+        st_agent(a.part + 2 * i, valid ? l - lg[a.s_off + i] : 0.f);
+        st_agent(a.part + 2 * i + 1, valid ? 1.f : 0.f);
     }
     if (!last_arrival(a.counter, gridDim.x)) return;
     double s0 = 0.0, s1 = 0.0;
@@ -517,81 +475,56 @@ __device__ __forceinline__ void normalize_bwd(const ContrastArgs& a, const float
         out[c] = clamped ? dxh[c] * inv : (dxh[c] - x[c] * inv * p) * inv;
 }
 
-// drow[r][c] = sum_k dl[r][k] * M[k][c] over k ascending (thread per column; M read once per R rows)
-template <int R>
-__device__ __forceinline__ void rows_times(const float* dl, int lddl, int nk, const float* M, int C, int nr,
-                                           float* drow) {
-    for (int c = threadIdx.x; c < C; c += LT) {
-        float acc[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = 0.f;
-        for (int k = 0; k < nk; ++k) {
-            const float m = M[(size_t)k * C + c];
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (r < nr) acc[r] += dl[r * lddl + k] * m;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (r < nr) drow[r * C + c] = acc[r];
-    }
-}
-
-// workgroups [0, nbt): groups of R t rows; [nbt, nbt + nbs): groups of R of this rank's s rows (when ds != NULL)
-template <int R>
+// workgroups [0, n): t rows; [n, n + n_local): this rank's s rows (when ds != NULL)
 __global__ __launch_bounds__(LT) void contrast_bwd_kernel(ContrastArgs a) {
-    extern __shared__ float lds[];           // [R][C] rows, [R][C] d rows, [R][max(n, n_all)] dlogits
+    extern __shared__ float lds[];           // [C] row, [C] d row, [max(n, n_all)] dlogits
     __shared__ float shf[LT];
     __shared__ double shd[LT];
-    const int W = a.n > a.n_all ? a.n : a.n_all;
     float* row = lds;
-    float* drow = lds + R * a.C;
-    float* dl = lds + 2 * R * a.C;
+    float* drow = lds + a.C;
+    float* dl = lds + 2 * a.C;
     const int t = threadIdx.x;
-    const int nbt = (a.n + R - 1) / R;
     // number of valid rows (the CE mean's denominator)
     float nv = 0.f;
     for (int q = t; q < a.n; q += LT) nv += a.src_labels[q] != -1 ? 1.f : 0.f;
     nv = block_sum(nv, shf);
     const float gsc = a.g[0] / nv;
-    if ((int)blockIdx.x < nbt) {
-        const int i0 = blockIdx.x * R, nr = min(R, a.n - i0);
-        logits_rows<R>(a, i0, nr, row, dl);     // row = t rows, dl[r] = logits rows (stride n_all)
-        for (int e = t; e < nr * a.n_all; e += LT) {
-            const int r = e / a.n_all, j = e - r * a.n_all, i = i0 + r;
-            const bool valid = a.src_labels[i] != -1;
-            dl[e] = valid ? gsc * (expf(dl[e] - a.lse[i]) - (j == a.s_off + i ? 1.f : 0.f)) * a.scale * a.inv[a.n + j]
-                          : 0.f;
-        }
+    if ((int)blockIdx.x < a.n) {
+        const int i = blockIdx.x;
+        logits_row(a, i, row, dl);           // row = t_i, dl = logits
+        const bool valid = a.src_labels[i] != -1;
+        const float l = a.lse[i];
+        for (int j = t; j < a.n_all; j += LT)
+            dl[j] = valid ? gsc * (expf(dl[j] - l) - (j == a.s_off + i ? 1.f : 0.f)) * a.scale * a.inv[a.n + j] : 0.f;
         __syncthreads();
         // d t_hat_i = sum_j dl_j * s_j   (dl already carries scale * inv_s_j)
-        rows_times<R>(dl, a.n_all, a.n_all, a.s, a.C, nr, drow);
+        for (int c = t; c < a.C; c += LT) {
+            float acc = 0.f;
+            for (int j = 0; j < a.n_all; ++j) acc += dl[j] * a.s[(size_t)j * a.C + c];
+            drow[c] = acc;
+        }
         __syncthreads();
-        for (int r = 0; r < nr; ++r)
-            normalize_bwd(a, row + r * a.C, a.inv[i0 + r], drow + r * a.C, a.dt + (size_t)(i0 + r) * a.C, shf);
+        normalize_bwd(a, row, a.inv[i], drow, a.dt + (size_t)i * a.C, shf);
         return;
     }
-    const int jl0 = (blockIdx.x - nbt) * R, nr = min(R, a.n - jl0), j0 = a.s_off + jl0;
-    for (int e = t; e < nr * a.C; e += LT) row[e] = a.s[(size_t)j0 * a.C + e];
+    const int jl = blockIdx.x - a.n, j = a.s_off + jl;
+    for (int c = t; c < a.C; c += LT) row[c] = a.s[(size_t)j * a.C + c];
     __syncthreads();
-    // columns j0 .. j0+nr-1 of the logits and their gradients, for every t row i
+    const float isj = a.inv[a.n + j];
+    // column j of the logits and its gradient, for every t row i
     for (int i = t; i < a.n; i += LT) {
-        float dots[R];
-        row_dots<R>(row, a.C, a.t + (size_t)i * a.C, a.C, nr, dots);
+        const float lg = row_dot(row, a.t + (size_t)i * a.C, a.C) * a.inv[i] * a.scale * isj;
         const bool valid = a.src_labels[i] != -1;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (r >= nr) break;
-            const int j = j0 + r;
-            const float lg = dots[r] * a.inv[i] * a.scale * a.inv[a.n + j];
-            dl[r * W + i] = valid ? gsc * (expf(lg - a.lse[i]) - (j == a.s_off + i ? 1.f : 0.f)) * a.scale * a.inv[i] : 0.f;
-        }
+        dl[i] = valid ? gsc * (expf(lg - a.lse[i]) - (j == a.s_off + i ? 1.f : 0.f)) * a.scale * a.inv[i] : 0.f;
     }
     __syncthreads();
-    rows_times<R>(dl, W, a.n, a.t, a.C, nr, drow);
+    for (int c = t; c < a.C; c += LT) {
+        float acc = 0.f;
+        for (int i = 0; i < a.n; ++i) acc += dl[i] * a.t[(size_t)i * a.C + c];
+        drow[c] = acc;
+    }
     __syncthreads();
-    for (int r = 0; r < nr; ++r)
-        normalize_bwd(a, row + r * a.C, a.inv[a.n + j0 + r], drow + r * a.C, a.ds + (size_t)(jl0 + r) * a.C, shf);
+    normalize_bwd(a, row, isj, drow, a.ds + (size_t)jl * a.C, shf);
     (void)shd;
 }
 
@@ -734,13 +667,8 @@ int ured_contrast_fwd(const float* t, const float* s_all, const long long* src_l
     ContrastArgs a = contrast_args(n, n_all, C, s_off, scale, t, s_all, src_labels, inv, lse);
     a.part = ws; a.counter = counter; a.loss = loss;
     hipLaunchKernelGGL(contrast_norms_kernel, dim3(n + n_all), dim3(LT), 0, (hipStream_t)stream, a);
-    const size_t lds_r = (size_t)CT_ROWS * (C + n_all) * sizeof(float);
-    if (CT_ROWS > 1 && lds_r <= 65536)
-        hipLaunchKernelGGL(contrast_fwd_kernel<CT_ROWS>, dim3((n + CT_ROWS - 1) / CT_ROWS), dim3(LT), lds_r,
-                           (hipStream_t)stream, a);
-    else
-        hipLaunchKernelGGL(contrast_fwd_kernel<1>, dim3(n), dim3(LT), (size_t)(C + n_all) * sizeof(float),
-                           (hipStream_t)stream, a);
+    const size_t lds = (size_t)(C + n_all) * sizeof(float);
+    hipLaunchKernelGGL(contrast_fwd_kernel, dim3(n), dim3(LT), lds, (hipStream_t)stream, a);
     return ured::launch_status("ured_contrast_fwd");
 }
 
@@ -754,15 +682,8 @@ int ured_contrast_bwd(const float* t, const float* s_all, const long long* src_l
     ContrastArgs a = contrast_args(n, n_all, C, s_off, scale, t, s_all, src_labels, const_cast<float*>(inv),
                                    const_cast<float*>(lse));
     a.g = g; a.dt = dt; a.ds = ds;
-    const int W = n > n_all ? n : n_all;
-    const size_t lds_r = (size_t)CT_ROWS * (2 * C + W) * sizeof(float);
-    if (CT_ROWS > 1 && lds_r <= 65536) {
-        const int nb = (n + CT_ROWS - 1) / CT_ROWS;
-        hipLaunchKernelGGL(contrast_bwd_kernel<CT_ROWS>, dim3(nb + (ds ? nb : 0)), dim3(LT), lds_r, (hipStream_t)stream, a);
-    } else {
-        hipLaunchKernelGGL(contrast_bwd_kernel<1>, dim3(n + (ds ? n : 0)), dim3(LT), (size_t)(2 * C + W) * sizeof(float),
-                           (hipStream_t)stream, a);
-    }
+    const size_t lds = (size_t)(2 * C + (n > n_all ? n : n_all)) * sizeof(float);
+    hipLaunchKernelGGL(contrast_bwd_kernel, dim3(n + (ds ? n : 0)), dim3(LT), lds, (hipStream_t)stream, a);
     return ured::launch_status("ured_contrast_bwd");
 }
 
