@@ -144,7 +144,10 @@ def test_deformnet_node_major_equals_channel_first(dev, C, seed):
     node set whose ReLU output is one row barely above zero (variance << eps, invstd ~ 300), where
     the reference's gradient is discontinuous and any fp32 summation order may land on either
     side (tools/deformnet_diag.py; ours is within the fp32 reference's error on every other seed
-    tried, with half its median error)."""
+    tried, with half its median error). The key projection's bias has an exactly zero gradient (the
+    softmax is invariant to a per-row logit shift, and q . b_k shifts every logit of a row alike):
+    both fp32 runs return rounding noise there, compared against a noise floor of 1e-6 of the
+    largest float64 parameter gradient instead of against each other."""
     import copy
     from network.deformation_net import DeformNet_MatchingNet
     torch.manual_seed(C + seed)
@@ -165,18 +168,22 @@ def test_deformnet_node_major_equals_channel_first(dev, C, seed):
     rout.backward(go)
     tout.backward(go.double())
 
-    def check(x, r, t, what):
+    def check(x, r, t, what, floor=0.0):
         e_ours, e_ref = _err(x, t), _err(r, t)
-        assert e_ours <= 3.0 * e_ref + 1e-5 * t.detach().abs().max().item() + 1e-9, (what, e_ours, e_ref)
+        assert e_ours <= 3.0 * e_ref + 1e-5 * t.detach().abs().max().item() + 1e-9 + floor, (what, e_ours, e_ref)
     check(out, rout, tout, "out")
     check(a_t.grad, b_t.grad, c_t.grad, "target_f grad")
     check(a_s.grad, b_s.grad, c_s.grad, "src_part_f grad")
     rp, tp = dict(ref.named_parameters()), dict(ref64.named_parameters())
+    gmax = max(v.grad.abs().max().item() for v in tp.values() if v.grad is not None)
     for k, p in net.named_parameters():
         if p.grad is None:
             assert rp[k].grad is None, k
             continue
-        check(p.grad, rp[k].grad, tp[k].grad, k)
+        zero = k.endswith("in_proj_k.bias")          # exactly zero in exact arithmetic (docstring)
+        if zero:
+            assert tp[k].grad.abs().max().item() <= 1e-12 * gmax, k
+        check(p.grad, rp[k].grad, tp[k].grad, k, floor=1e-6 * gmax if zero else 0.0)
     rb, tb = dict(ref.named_buffers()), dict(ref64.named_buffers())
     for k, v in net.named_buffers():
         if v.dtype.is_floating_point:
