@@ -859,6 +859,9 @@ constexpr int PRO_LDS = 1024;            // max prologue channels staged in LDS 
 #define URED_DMA_SPREAD 2
 #endif
 constexpr int BUF_DWORD3 = 0x00020000;   // raw buffer, gfx9 family (gfx950)
+#ifndef URED_EXP_DGRAD_PRO
+#define URED_EXP_DGRAD_PRO 0
+#endif
 
 __host__ __device__ inline bool buf_ok(const UredGemmDesc& d) {
     // a concatenated second A source must start on a K-step boundary (one descriptor per step)
@@ -1823,6 +1826,11 @@ int dispatch(const UredGemmDesc& d, hipStream_t st) {
         // dgrad
         URED_CASE(0, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_BNBWD)
         URED_CASE(0, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_STORE)
+#if URED_EXP_DGRAD_PRO
+        // measurement build only (tools/gemm_bench.py dgrad_bnbwd_pro): the BN-backward dgrad with the
+        // forward's one-input A prologue, the lower bound of folding the BN-backward apply into it
+        URED_CASE(0, 1, URED_PRO_ENC, URED_PRO_NONE, URED_EPI_BNBWD)
+#endif
         // few output tiles, long K (per-group codes, fc layers): split-K partials
         URED_CASE(0, 0, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_SPLITK)
         URED_CASE(0, 1, URED_PRO_NONE, URED_PRO_NONE, URED_EPI_SPLITK)

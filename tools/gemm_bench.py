@@ -72,6 +72,7 @@ def main():
         bws = torch.empty(K.nblocks(M), 2, Kd, device=dev)
         st = K.BNState(torch.zeros(Kd, device=dev), torch.ones(Kd, device=dev), s, t)
         dW = torch.empty(N, Kd, device=dev)
+        t2 = torch.rand(N, device=dev, generator=g) + 0.5      # prologue scale / shift over the dgrad's K = N
         flop = 2.0 * M * N * Kd
         r = {}
         r["fwd"] = flop / timeit(lambda: K.gemm(M, N, Kd, X, Kd, W, Kd, Y, N, pro_a=K.PRO_ENC, pro_s=s, pro_t=t,
@@ -83,6 +84,12 @@ def main():
                                          a.iters) / 1e12
         r["dgrad_bnbwd"] = flop / timeit(lambda: K.gemm(M, Kd, N, dY, N, W, Kd, G, Kd, b_kmajor=True, epi=K.EPI_BNBWD,
                                                         Yp=X, ldy=Kd, bn=st, bwd_ws=bws), a.iters) / 1e12
+        try:   # measurement build only (-DURED_EXP_DGRAD_PRO=1): the dgrad with a one-input A prologue
+            r["dgrad_bnbwd_pro"] = flop / timeit(lambda: K.gemm(M, Kd, N, dY, N, W, Kd, G, Kd, b_kmajor=True,
+                                                                epi=K.EPI_BNBWD, Yp=X, ldy=Kd, bn=st, bwd_ws=bws,
+                                                                pro_a=K.PRO_ENC, pro_s=t2, pro_t=t2), a.iters) / 1e12
+        except Exception:
+            pass
         if a.dgrad_layouts:
             Wt = W.t().contiguous()   # [Kd][N]: the dgrad B operand row-major (k = N contiguous)
             r["dgrad_store"] = flop / timeit(lambda: K.gemm(M, Kd, N, dY, N, W, Kd, G, Kd, b_kmajor=True), a.iters) / 1e12
