@@ -71,11 +71,8 @@ def _worker(port, q):
         def params(step):
             return {(m, k): p.detach().clone() for m in step.models for k, p in step.models[m].named_parameters()}
 
-        # one stream order everywhere: the single-process references would otherwise run DeformNet on
-        # its side stream (engine/train.py _deform_stream), whose backward adds some gradient
-        # contributions in another order than the data-parallel steps (which keep one stream)
-        cfg1 = dict(CFG, use_contrast_loss=0.0, cuda_graph=True, deform_overlap=False)
-        cfg2 = dict(CFG, cuda_graph=True, differentiable_gather=True, deform_overlap=False)
+        cfg1 = dict(CFG, use_contrast_loss=0.0, cuda_graph=True)
+        cfg2 = dict(CFG, cuda_graph=True, differentiable_gather=True)
         ref1 = make(TrainStep, cfg1)
         l_ref1, p_ref1 = run(ref1), params(ref1)
         ref2 = make(TrainStep, cfg2)
