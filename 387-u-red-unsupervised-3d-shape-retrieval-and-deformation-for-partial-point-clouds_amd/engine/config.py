@@ -43,8 +43,6 @@ EXTRA = {
     "log_every", "compute_connectivity", "src_connectivity_plane", "synthetic_targets", "differentiable_gather", "sync_bn", "loss_head", "dist_backend",
     # data parallel (engine/dp.py, engine/graph.py)
     "dp_bucket_mb", "dp_last_bucket_mb", "dp_force_collectives", "graph_inline_collectives",
-    # single-process overlap (engine/train.py _deform_stream)
-    "deform_overlap",
 }
 
 TRAIN_REQUIRED = ("source_latent_dim", "target_latent_dim", "sem_latent_dim", "MAX_NUM_PARTS", "device",

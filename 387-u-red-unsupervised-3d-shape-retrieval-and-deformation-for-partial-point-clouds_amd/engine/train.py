@@ -55,7 +55,6 @@ from ured_hip.kernels import RowWeights  # noqa: E402
 from ured_hip.ops import PartBounds, UniqueRows, build_parts, part_aabb, part_rows, upload  # noqa: E402
 
 _SHAPE_SRC = os.environ.get("URED_SHAPE_SRC", "1") == "1"     # A/B knob (tools/gpu_py_ab.sh)
-_DEFORM_OVERLAP = os.environ.get("URED_DEFORM_OVERLAP", "1") == "1"   # default of cfg "deform_overlap"
 
 MODULE_NAMES = ("target_encoder_full", "param_decoder_full", "recon_decoder_full", "re_residual_net_full",
                 "src_encoder_all", "recon_decoder_src", "embedding_layer")
@@ -254,31 +253,13 @@ class TrainStep:
         target_part_f, _, re_in, mask_part, parts, param_def, pp_alias = get_part(cfg, pp.view(B, N, -1),
                                                                                  batch["labels"], x, alias=True)
         codes = codes.view(B, P, -1)
-        dside = self._deform_stream(x.device)
-        if dside is not None:
-            # DeformNet + get_shape (chains of latency-bound small kernels) on their own stream, beside
-            # the reconstruction decoder and the residual net (independent of them); autograd runs
-            # each backward node on its forward's stream, so the two overlap in the backward too
-            main = torch.cuda.current_stream(x.device)
-            dside.wait_stream(main)
-            for t in (tcode, codes, param_def, src_labels):
-                t.record_stream(dside)          # main-stream tensors the side stream reads
-            with torch.cuda.stream(dside):
-                params_full = M["param_decoder_full"](tcode, codes, None)
-                out = (get_shape_src(self.db, src_labels, params_full, param_def, cfg["alpha"]) if _SHAPE_SRC else
-                       get_shape(mats, params_full, param_def, cfg["alpha"])).reshape(B, -1, 3)
-        else:
-            params_full = M["param_decoder_full"](tcode, codes, None)
-            out = (get_shape_src(self.db, src_labels, params_full, param_def, cfg["alpha"]) if _SHAPE_SRC else
-                   get_shape(mats, params_full, param_def, cfg["alpha"])).reshape(B, -1, 3)
+        params_full = M["param_decoder_full"](tcode, codes, None)
+        out = (get_shape_src(self.db, src_labels, params_full, param_def, cfg["alpha"]) if _SHAPE_SRC else
+               get_shape(mats, params_full, param_def, cfg["alpha"])).reshape(B, -1, 3)
         recon_full_p = M["recon_decoder_full"].forward_split(pp_alias.view(B * N, -1), tcode,
                                                              group_rows=N).view(B, N, 3)
         re_res = M["re_residual_net_full"].forward_split(re_in.pp_sorted, re_in.part_mean, gidx=re_in.gid,
                                                          off=re_in.off).view(B, N, 3)
-        if dside is not None:
-            main.wait_stream(dside)
-            out.record_stream(main)             # side-stream tensors the main stream reads
-            params_full.record_stream(main)
         param = regularization_param(params_full, mask_part) if cfg.get("use_param_loss", 0.0) > 0.0 else None
         contrast_ext = None
         if gathers(self.force_gather) and cfg.get("use_contrast_loss", 0.0) > 0.0:
@@ -376,19 +357,6 @@ class TrainStep:
         self.reduce_gradients()
         self.clip_and_step()
         return T
-
-    def _deform_stream(self, device):
-        """The DeformNet side stream (cfg "deform_overlap", default on for a single process on a GPU
-        without SyncBN: its collectives and the data-parallel bucket hooks keep one stream order)."""
-        import torch.distributed as dist
-        on = self.cfg.get("deform_overlap", _DEFORM_OVERLAP)
-        if (not on or device.type != "cuda" or self.sync_bn or
-                (dist.is_initialized() and dist.get_world_size() > 1) or getattr(self, "collect", False)):
-            return None
-        s = getattr(self, "_dside", None)
-        if s is None or s.device != device:
-            s = self._dside = torch.cuda.Stream(device=device)
-        return s
 
     def backward_loss(self, loss):
         """loss.backward() seeded with a persistent 1.0 (no fill kernel per step; a HIP-graph
