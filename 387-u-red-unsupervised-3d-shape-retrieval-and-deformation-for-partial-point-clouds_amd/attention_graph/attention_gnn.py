@@ -119,29 +119,20 @@ class ResidualAttentionMessagePropagation(nn.Module):
     def _node_ffn_ok(self):
         return self.fc.use_norm == "use_bn" and len(self.fc) == 4
 
-    def node_pair_ok(self):
-        """forward_nodes_self_pair runs the fused node-major path (softmax attention, BN FFN)."""
-        return self.mha.attention_func is softmax_attention and self._node_ffn_ok()
-
-    def forward_nodes_self_pair(self, x0, x1, X=None, n0=None):
+    def forward_nodes_self_pair(self, x0, x1):
         """(forward_nodes(x0), forward_nodes(x1)) — the two self-attention calls of a
         DescriptorsSelfAttention layer (shared weights) — with every node GEMM run once over
         the rows of both node sets, and both sets' attention in one launch (ured_hip.attn
         SelfAttnPairFn): the attention and the BatchNorm still see one set at a time (per-set
         batch statistics, running stats updated set 0 then set 1), so the values are those of the
-        two calls; half the launches, no gradient accumulation across calls. X (optional): the
-        two sets already as one row block [B*n0 + B*n1, C] (ured_hip.attn.graph_nodes); x0 may then
-        be None, with its node count in n0."""
+        two calls; half the launches, no gradient accumulation across calls."""
         mha = self.mha
-        if not self.node_pair_ok():
-            if X is not None:
-                raise ValueError("forward_nodes_self_pair: a row-block input needs the node-major HIP path")
+        if mha.attention_func is not softmax_attention or not self._node_ffn_ok():
             return self.forward_nodes(x0), self.forward_nodes(x1)
-        B, n1, C = x1.shape
-        n0 = x0.shape[1] if x0 is not None else int(n0)
+        B, n0, C = x0.shape
+        n1 = x1.shape[1]
         R0, R1 = B * n0, B * n1
-        if X is None:
-            X = torch.cat([x0.reshape(R0, C), x1.reshape(R1, C)])
+        X = torch.cat([x0.reshape(R0, C), x1.reshape(R1, C)])
         q_, k_, v_ = mha.in_proj_q, mha.in_proj_k, mha.in_proj_v
         # X's second consumer (the FFN) reads the projection's alias of it (NodeProjFn)
         qkv = node_proj((X,), [(mha._w(q_), mha._w(k_), mha._w(v_))], [(q_.bias, k_.bias, v_.bias)],
@@ -169,8 +160,8 @@ class DescriptorsSelfAttention(nn.Module):
     def forward(self, desc0, desc1):
         return self.module(desc0, desc0), self.module(desc1, desc1)
 
-    def forward_nodes(self, desc0, desc1, X=None, n0=None):
-        return self.module.forward_nodes_self_pair(desc0, desc1, X, n0)
+    def forward_nodes(self, desc0, desc1):
+        return self.module.forward_nodes_self_pair(desc0, desc1)
 
 
 class DescriptorsCrossAttention(nn.Module):
@@ -203,18 +194,8 @@ class GraphAttentionNet(nn.Module):
             desc0, desc1 = layer(desc0, desc1)
         return desc0, desc1
 
-    def forward_nodes(self, desc0, desc1, X0=None, n0=None):
-        """Node-major [B, n0, C], [B, n1, C]. X0 (optional, see accepts_row_block): both input sets
-        as one row block for the first (self-attention) layer; desc0 may then be None."""
-        for i, layer in enumerate(self.layers):
-            if i == 0 and X0 is not None:
-                desc0, desc1 = layer.forward_nodes(desc0, desc1, X=X0, n0=n0)
-            else:
-                desc0, desc1 = layer.forward_nodes(desc0, desc1)
+    def forward_nodes(self, desc0, desc1):
+        """Node-major [B, n0, C], [B, n1, C]."""
+        for layer in self.layers:
+            desc0, desc1 = layer.forward_nodes(desc0, desc1)
         return desc0, desc1
-
-    def accepts_row_block(self):
-        """The first layer is a self-attention layer on the node-major HIP path, so forward_nodes
-        can take its two input sets as one row block (X0)."""
-        return (len(self.layers) > 0 and isinstance(self.layers[0], DescriptorsSelfAttention)
-                and self.layers[0].module.node_pair_ok())

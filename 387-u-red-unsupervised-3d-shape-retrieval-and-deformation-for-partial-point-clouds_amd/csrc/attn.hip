@@ -189,50 +189,6 @@ size_t fwd_lds(int n, int m, int d) { return sizeof(float) * ((size_t)(n + 2 * m
 size_t bwd_lds(int n, int m, int d) { return sizeof(float) * ((size_t)(2 * n + 2 * m) * (d + 1) + 2 * (size_t)n * m); }
 
 
-// DeformNet's graph input (network/deformation_net.py:74-80): the global nodes
-// stack([mean over parts, target code]) followed by the part nodes, as ONE [2B + B*P, C] row
-// block (the first DescriptorsSelfAttention layer reads both node sets from it): row 2b = mean_p
-// parts[b, p] (sum in p order, times 1/P as torch's mean), row 2b+1 = target[b], row 2B + b*P + p =
-// parts[b, p]. The backward: dparts = dX[part row] + dX[2b] / P (MeanBackward), dtarget = dX[2b+1].
-__global__ __launch_bounds__(256) void graph_nodes_fwd_kernel(const float* __restrict__ parts,
-        const float* __restrict__ target, int B, int P, int C, float* __restrict__ X) {
-    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-    const long long total = (long long)B * (2 + P) * C;
-    if (e >= total) return;
-    const long long row = e / C;
-    const int c = (int)(e - row * C);
-    float v;
-    if (row < 2LL * B) {
-        const int b = (int)(row >> 1);
-        if (row & 1) {
-            v = target[(size_t)b * C + c];
-        } else {
-            const float* pb = parts + (size_t)b * P * C + c;
-            float s = 0.f;
-            for (int p = 0; p < P; ++p) s += pb[(size_t)p * C];
-            v = s * (1.0f / (float)P);
-        }
-    } else {
-        v = parts[(size_t)(row - 2LL * B) * C + c];
-    }
-    X[e] = v;
-}
-
-__global__ __launch_bounds__(256) void graph_nodes_bwd_kernel(const float* __restrict__ dX, int B, int P, int C,
-        float* __restrict__ dparts, float* __restrict__ dtarget) {
-    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-    const long long np = (long long)B * P * C;
-    if (e < np) {
-        const long long r = e / C;                   // part row b*P + p
-        const int c = (int)(e - r * C), b = (int)(r / P);
-        dparts[e] = dX[(size_t)(2LL * B + r) * C + c] + dX[(size_t)(2 * b) * C + c] / (float)P;
-    } else if (e < np + (long long)B * C) {
-        const long long q = e - np;
-        const int b = (int)(q / C), c = (int)(q - (long long)b * C);
-        dtarget[q] = dX[(size_t)(2 * b + 1) * C + c];
-    }
-}
-
 // Validate one set and add it to the launch table (B == 0 sets add no workgroups).
 int add_set(const char* who, bool bwd, const UredAttnSet& x, AttnSets& S, size_t& lds) {
     if (int rc = check_sizes(who, x.B, x.H, x.n, x.m, x.d)) return rc;
@@ -295,28 +251,6 @@ int ured_attn_bwd(const float* q, int ldq, const float* k, int ldk, const float*
     const UredAttnSet x{q, ldq, k, ldk, v, ldv, B, H, n, m, d, scale, nullptr, 0, const_cast<float*>(weights),
                         dout, lddo, dq, lddq, dk, lddk, dv, lddv};
     return launch_sets("ured_attn_bwd", true, 1, &x, stream);
-}
-
-int ured_graph_nodes_fwd(const float* parts, const float* target, int B, int P, int C, float* X, void* stream) {
-    ured::clear_error();
-    URED_REQUIRE(B >= 0 && P > 0 && C > 0, "ured_graph_nodes_fwd: bad sizes B=%d P=%d C=%d", B, P, C);
-    if (B == 0) return 0;
-    URED_REQUIRE(parts && target && X, "ured_graph_nodes_fwd: null pointer");
-    const long long total = (long long)B * (2 + P) * C;
-    hipLaunchKernelGGL(graph_nodes_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, parts, target, B, P, C, X);
-    return ured::launch_status("ured_graph_nodes_fwd");
-}
-
-int ured_graph_nodes_bwd(const float* dX, int B, int P, int C, float* dparts, float* dtarget, void* stream) {
-    ured::clear_error();
-    URED_REQUIRE(B >= 0 && P > 0 && C > 0, "ured_graph_nodes_bwd: bad sizes B=%d P=%d C=%d", B, P, C);
-    if (B == 0) return 0;
-    URED_REQUIRE(dX && dparts && dtarget, "ured_graph_nodes_bwd: null pointer");
-    const long long total = (long long)B * (P + 1) * C;
-    hipLaunchKernelGGL(graph_nodes_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, dX, B, P, C, dparts, dtarget);
-    return ured::launch_status("ured_graph_nodes_bwd");
 }
 
 int ured_attn_fwd_sets(int nsets, const UredAttnSet* sets, void* stream) {

@@ -6,18 +6,13 @@ ured_hip.mlp.ResidualNetFn; DeformNet_MatchingNet (2 + MAX_NUM_PARTS graph nodes
 runs its graph attention and param_decoder on the node kernels of csrc/node.hip
 (ured_hip.node) and csrc/attn.hip.
 """
-import os
-
 import torch
 import torch.nn as nn
 
 from attention_graph.attention_gnn import GraphAttentionNet
 from attention_graph.attention_utils import FeedForwardNet_norm
 from ured_hip.mlp import ResidualNetFn
-from ured_hip.attn import graph_nodes
 from ured_hip.node import param_decoder as node_param_decoder
-
-_GRAPH_NODES = os.environ.get("URED_GRAPH_NODES", "1") == "1"    # A/B knob (tools/gpu_py_ab.sh)
 
 
 class DeformNet_MatchingNet(nn.Module):
@@ -49,14 +44,8 @@ class DeformNet_MatchingNet(nn.Module):
         (same values; channel-first views are never materialised)."""
         bs = target_f.shape[0]
         parts = src_part_f.reshape(bs, src_part_f.shape[1], -1)                        # [B, P, C]
-        gat = self.graph_attention_net
-        if _GRAPH_NODES and parts.is_cuda and gat.accepts_row_block():
-            # [mean part, target] global nodes and the part nodes as one row block, one launch
-            # each way (ured_hip.attn.graph_nodes), read in place by the first self-attention layer
-            nodes, parts = gat.forward_nodes(None, parts, X0=graph_nodes(parts, target_f), n0=2)
-        else:
-            nodes = torch.stack([parts.mean(dim=1), target_f], dim=1)                  # [B, 2, C]
-            nodes, parts = gat.forward_nodes(nodes, parts)
+        nodes = torch.stack([parts.mean(dim=1), target_f], dim=1)                      # [B, 2, C]
+        nodes, parts = self.graph_attention_net.forward_nodes(nodes, parts)
         P = parts.shape[1]
         if self.param_decoder.use_norm in ("None", None) and len(self.param_decoder) == 3:
             # cat([g0 | g1 broadcast to the parts, parts]): the global half as a per-sample row bias

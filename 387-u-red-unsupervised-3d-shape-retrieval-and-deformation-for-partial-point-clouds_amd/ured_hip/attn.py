@@ -30,8 +30,6 @@ _lib.register({
     "ured_attn_bwd": [_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _I, _P, _I, _P, _I, _P],
     "ured_attn_fwd_sets": [_I, _P, _P],
     "ured_attn_bwd_sets": [_I, _P, _P],
-    "ured_graph_nodes_fwd": [_P, _P, _I, _I, _I, _P, _P],
-    "ured_graph_nodes_bwd": [_P, _I, _I, _I, _P, _P, _P],
 })
 
 
@@ -157,39 +155,6 @@ def _sets(qkv, out, w, bwd, B, n0, n1, heads, C, d):
             x.dout, x.lddo = dout.data_ptr() + 4 * row0[i] * C, C
             x.dq, x.lddq, x.dk, x.lddk, x.dv, x.lddv = g, ld, g + 4 * C, ld, g + 8 * C, ld
     return arr
-
-
-class GraphNodesFn(Function):
-    """DeformNet's graph input as one row block: X [2B + B*P, C] = [per sample: mean of its part
-    nodes, its target code] then every part node (network/deformation_net.py:74-80: stack + mean,
-    and the concatenation the first self-attention layer reads). One launch each way in place of
-    mean / stack / cat forward and the mean / stack backward's div and adds."""
-
-    @staticmethod
-    def forward(ctx, parts, target):
-        _lib.require_device(parts, target)
-        parts, target = parts.contiguous().float(), target.contiguous().float()
-        B, P, C = parts.shape
-        X = torch.empty(B * (2 + P), C, device=parts.device)
-        _lib.call("ured_graph_nodes_fwd", parts.data_ptr(), target.data_ptr(), B, P, C, X.data_ptr(),
-                  _lib.stream_of(X))
-        ctx.dims = (B, P, C)
-        return X
-
-    @staticmethod
-    def backward(ctx, dX):
-        B, P, C = ctx.dims
-        dX = dX.contiguous()
-        dparts = torch.empty(B, P, C, device=dX.device)
-        dtarget = torch.empty(B, C, device=dX.device)
-        _lib.call("ured_graph_nodes_bwd", dX.data_ptr(), B, P, C, dparts.data_ptr(), dtarget.data_ptr(),
-                  _lib.stream_of(dX))
-        return dparts, dtarget
-
-
-def graph_nodes(parts, target):
-    """[B*2 + B*P, C] rows: (mean of parts[b], target[b]) for each b, then parts flattened."""
-    return GraphNodesFn.apply(parts, target)
 
 
 def self_attention(qkv, heads):

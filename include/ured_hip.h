@@ -40,7 +40,7 @@ extern "C" {
 #define URED_EINVAL 1001
 
 /* Library identification: returns URED_ABI_VERSION. */
-#define URED_ABI_VERSION 9   /* 9: ured_attn_fwd_sets / ured_attn_bwd_sets, ured_get_shape_src_fwd / _bwd, ured_graph_nodes_fwd / _bwd; 8: ured_nn_bwd_set; 7: ured_copy_batch; 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
+#define URED_ABI_VERSION 9   /* 9: ured_attn_fwd_sets / ured_attn_bwd_sets, ured_get_shape_src_fwd / _bwd; 8: ured_nn_bwd_set; 7: ured_copy_batch; 6: ured_part_rows_bwd_add; 5: node BN SyncBN fields (stats_out/stats_in, sums_out/sums_in); ured_bn_stats et al. */
 int ured_abi_version(void);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* ured_last_error(void);
@@ -377,13 +377,6 @@ typedef struct {
 } UredAttnSet;
 int ured_attn_fwd_sets(int nsets, const UredAttnSet* sets, void* stream);
 int ured_attn_bwd_sets(int nsets, const UredAttnSet* sets, void* stream);
-
-/* DeformNet's graph input (network/deformation_net.py:74-80: nodes = stack([parts.mean(1), target])
- * and the part nodes) as one row block X [2B + B*P, C]: rows 2b / 2b+1 = mean_p parts[b] (sum in
- * p order times 1/P) / target[b], rows 2B + b*P + p = parts[b, p]. Backward: dparts = dX[part row]
- * + dX[2b] / P, dtarget = dX[2b+1]. parts [B, P, C], target [B, C], all contiguous fp32. */
-int ured_graph_nodes_fwd(const float* parts, const float* target, int B, int P, int C, float* X, void* stream);
-int ured_graph_nodes_bwd(const float* dX, int B, int P, int C, float* dparts, float* dtarget, void* stream);
 
 /* ---------------- graph-node layers (DeformNet_MatchingNet, node.hip) ----------------
  * Replace the node-level Conv1d(k=1) layers (in_proj_q/k/v, out_proj, the FeedForwardNet_norm

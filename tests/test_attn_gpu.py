@@ -87,28 +87,6 @@ def test_self_attention_pair_equals_two_calls(dev, B, H, n0, n1, d):
     assert torch.equal(x.grad[:R0], x0.grad.reshape(R0, 3 * C)) and torch.equal(x.grad[R0:], x1.grad.reshape(R1, 3 * C))
 
 
-@pytest.mark.parametrize("B,P,C", [(16, 16, 512), (3, 5, 24)])
-def test_graph_nodes_matches_stack_mean_cat(dev, B, P, C):
-    """DeformNet's graph input row block (ured_graph_nodes_fwd/bwd) vs the torch composition it
-    replaces (stack([parts.mean(1), target]), cat with the parts): values and both gradients within
-    fp32 rounding (the mean's summation order is the kernel's own)."""
-    from ured_hip.attn import graph_nodes
-    g = torch.Generator().manual_seed(B + P)
-    parts = torch.randn(B, P, C, generator=g).to(dev)
-    target = torch.randn(B, C, generator=g).to(dev)
-    gX = torch.randn(B * (2 + P), C, generator=g).to(dev)
-    a, t = parts.clone().requires_grad_(True), target.clone().requires_grad_(True)
-    X = graph_nodes(a, t)
-    X.backward(gX)
-    b, u = parts.clone().requires_grad_(True), target.clone().requires_grad_(True)
-    ref = torch.cat([torch.stack([b.mean(dim=1), u], dim=1).reshape(2 * B, C), b.reshape(B * P, C)])
-    ref.backward(gX)
-    torch.testing.assert_close(X, ref, rtol=1e-6, atol=1e-6)
-    assert torch.equal(X[1:2 * B:2], ref[1:2 * B:2]) and torch.equal(X[2 * B:], ref[2 * B:])
-    torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-6)
-    assert torch.equal(t.grad, u.grad)
-
-
 def test_attention_rejects_oversize(dev):
     from ured_hip import _lib
     from ured_hip.attn import cross_attention
