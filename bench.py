@@ -792,13 +792,18 @@ def main():
                 for row in csv.DictReader(f):
                     if dom_key in row["Name"]:
                         prof_avg = float(row["AverageNs"]) * 1e-6
+        # the committed trace is of the default workload: a run of another size (e.g. the tests' small
+        # --batch) keeps its live figures (a >25 % mismatch with them marks another workload)
+        if prof_avg and abs(prof_avg / avg_ms - 1.0) > 0.25:
+            prof_avg = None
         if prof_avg:
             avg_ms, ach = prof_avg, flop_per_launch / (prof_avg * 1e-3) / 1e12
             timing = (f"rocprofv3 kernel-trace average of this kernel over the timed steps of the same command "
                       f"({os.path.relpath(prof, ROOT)})")
         traffic, tsrc = None, None
+        profiled = prof_avg is not None      # the profile files describe this run's workload
         pmc = os.path.join(ROOT, "profiles", PMC_SUMMARY)
-        if os.path.exists(pmc):
+        if profiled and os.path.exists(pmc):
             pm = json.load(open(pmc))
             for kname, v in pm.items():
                 if dom_key in kname:
@@ -810,7 +815,7 @@ def main():
                     "kernel": dom_key, "launches_per_step": round(lps, 2), "avg_launch_ms": round(avg_ms, 4),
                     "flop_per_launch": round(flop_per_launch), "timing": timing, "live_hip_events": live}
         clk = os.path.join(ROOT, "profiles", CLOCK_SUMMARY)
-        if os.path.exists(clk):
+        if profiled and os.path.exists(clk):
             for kname, v in json.load(open(clk)).items():
                 if dom_key in kname:
                     # the chip holds ~2.2 GHz under this MFMA load (DVFS): the peak at that clock
@@ -819,7 +824,7 @@ def main():
                     roofline["frac_at_held_clock"] = round(ach / (PEAK_FP32_TFLOPS * ghz / NOMINAL_GHZ), 4)
                     roofline["clock_source"] = os.path.relpath(clk, ROOT)
         sq = os.path.join(ROOT, "profiles", SQ_SUMMARY)
-        if os.path.exists(sq):
+        if profiled and os.path.exists(sq):
             for kname, v in json.load(open(sq)).items():
                 if dom_key in kname and v.get("GRBM_GUI_ACTIVE"):
                     # SQ_VALU_MFMA_BUSY_CYCLES over the 1024 SIMDs x the kernel's cycles
