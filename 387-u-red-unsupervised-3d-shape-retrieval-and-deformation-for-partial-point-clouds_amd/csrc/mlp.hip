@@ -1438,44 +1438,21 @@ __global__ __launch_bounds__(64 * BNF_WAVES) void bn_fwd_finalize_wave_kernel(co
     const int nblk = (M + BM - 1) / BM;
     const float* p0 = ws + part_idx(0, n, 0, N, M);
     const float* p1 = ws + part_idx(1, n, 0, N, M);
-    // the partials a lane needs (8 per 512 rows of blocks) are loaded together, then summed in order
-    constexpr int U = 8;
-    double s = 0.0, c = 0.0, q = 0.0;
-    for (int b0 = lane; b0 < nblk; b0 += 64 * U) {
-        float v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = b0 + 64 * u < nblk ? p0[b0 + 64 * u] : 0.f;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int b = b0 + 64 * u;
-            if (b < nblk) {
-                const double cnt = (double)min(BM, M - b * BM) * blk_weight(gw, grows, b);
-                s += cnt * (double)v[u];
-                c += cnt;
-            }
-        }
+    double s = 0.0, c = 0.0;
+    for (int b = lane; b < nblk; b += 64) {
+        const double cnt = (double)min(BM, M - b * BM) * blk_weight(gw, grows, b);
+        s += cnt * (double)p0[b];
+        c += cnt;
     }
     s = wave_sum_d(s);
     const double Mw = wave_sum_d(c);
     const double mean = s / Mw;
-    for (int b0 = lane; b0 < nblk; b0 += 64 * U) {
-        float v[U], m[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool ok = b0 + 64 * u < nblk;
-            v[u] = ok ? p0[b0 + 64 * u] : 0.f;
-            m[u] = ok ? p1[b0 + 64 * u] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int b = b0 + 64 * u;
-            if (b < nblk) {
-                const double w = blk_weight(gw, grows, b);
-                const double cnt = (double)min(BM, M - b * BM) * w;
-                const double dm = (double)v[u] - mean;
-                q += w * (double)m[u] + cnt * dm * dm;
-            }
-        }
+    double q = 0.0;
+    for (int b = lane; b < nblk; b += 64) {
+        const double w = blk_weight(gw, grows, b);
+        const double cnt = (double)min(BM, M - b * BM) * w;
+        const double dm = (double)p0[b] - mean;
+        q += w * (double)p1[b] + cnt * dm * dm;
     }
     const double m2 = wave_sum_d(q);
     if (lane == 0) {
@@ -1504,25 +1481,11 @@ __global__ __launch_bounds__(64 * BNF_WAVES) void bn_bwd_finalize_wave_kernel(co
     const int nblk = (M + BM - 1) / BM;
     const float* p0 = ws + part_idx(0, n, 0, N, M);
     const float* p1 = ws + part_idx(1, n, 0, N, M);
-    constexpr int U = 8;
     double a = 0.0, b = 0.0, c = 0.0;
-    for (int k0 = lane; k0 < nblk; k0 += 64 * U) {
-        float v[U], m[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool ok = k0 + 64 * u < nblk;
-            v[u] = ok ? p0[k0 + 64 * u] : 0.f;
-            m[u] = ok ? p1[k0 + 64 * u] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int k = k0 + 64 * u;
-            if (k < nblk) {
-                a += (double)v[u];
-                b += (double)m[u];
-                c += (double)min(BM, M - k * BM) * blk_weight(gw, grows, k);
-            }
-        }
+    for (int k = lane; k < nblk; k += 64) {
+        a += (double)p0[k];
+        b += (double)p1[k];
+        c += (double)min(BM, M - k * BM) * blk_weight(gw, grows, k);
     }
     const double db = wave_sum_d(a), dg = wave_sum_d(b), Mw = wave_sum_d(c);
     if (lane == 0) {
