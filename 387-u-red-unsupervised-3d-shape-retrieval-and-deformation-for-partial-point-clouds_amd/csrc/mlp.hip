@@ -1412,93 +1412,6 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
 }
 
 // rows in blocks of 128 (matches the partial layout), 256 threads = columns
-// Round-6 form (URED_BN_FIN_WAVE, default): ONE wave per column, four columns per workgroup. A
-// column's partial rows are contiguous (part_idx), so a lane reads every 64th of them with its loads
-// in flight together and the wave combines its lanes with an fp64 xor butterfly (no LDS tree and
-// no workgroup barriers on the latency path of these short, dependent reductions).
-#ifndef URED_BN_FIN_WAVE
-#define URED_BN_FIN_WAVE 1
-#endif
-constexpr int BNF_WAVES = 4;
-
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-__global__ __launch_bounds__(64 * BNF_WAVES) void bn_fwd_finalize_wave_kernel(const float* __restrict__ ws, int M, int N,
-        const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
-        float* running_mean, float* running_var, float* mean_o, float* invstd_o, float* scale_o, float* shift_o,
-        const float* __restrict__ gw, int grows, long long* nbt) {
-    const int lane = threadIdx.x & 63;
-    const int n = blockIdx.x * BNF_WAVES + (threadIdx.x >> 6);
-    if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
-    if (n >= N) return;                        // whole wave
-    const int nblk = (M + BM - 1) / BM;
-    const float* p0 = ws + part_idx(0, n, 0, N, M);
-    const float* p1 = ws + part_idx(1, n, 0, N, M);
-    double s = 0.0, c = 0.0;
-    for (int b = lane; b < nblk; b += 64) {
-        const double cnt = (double)min(BM, M - b * BM) * blk_weight(gw, grows, b);
-        s += cnt * (double)p0[b];
-        c += cnt;
-    }
-    s = wave_sum_d(s);
-    const double Mw = wave_sum_d(c);
-    const double mean = s / Mw;
-    double q = 0.0;
-    for (int b = lane; b < nblk; b += 64) {
-        const double w = blk_weight(gw, grows, b);
-        const double cnt = (double)min(BM, M - b * BM) * w;
-        const double dm = (double)p0[b] - mean;
-        q += w * (double)p1[b] + cnt * dm * dm;
-    }
-    const double m2 = wave_sum_d(q);
-    if (lane == 0) {
-        const double var = m2 / Mw;
-        const float is = (float)(1.0 / sqrt(var + (double)eps));
-        const float mf = (float)mean;
-        mean_o[n] = mf;
-        invstd_o[n] = is;
-        const float sc = gamma ? gamma[n] * is : is;
-        scale_o[n] = sc;
-        shift_o[n] = (beta ? beta[n] : 0.f) - mf * sc;
-        if (running_mean) running_mean[n] = (1.f - momentum) * running_mean[n] + momentum * mf;
-        if (running_var) {
-            const float uv = (float)(Mw > 1.0 ? m2 / (Mw - 1.0) : m2);
-            running_var[n] = (1.f - momentum) * running_var[n] + momentum * uv;
-        }
-    }
-}
-
-__global__ __launch_bounds__(64 * BNF_WAVES) void bn_bwd_finalize_wave_kernel(const float* __restrict__ ws, int M, int N,
-        const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma, float* dbeta, int accumulate,
-        float* ca, float* cb, float* cc, const float* __restrict__ gw, int grows) {
-    const int lane = threadIdx.x & 63;
-    const int n = blockIdx.x * BNF_WAVES + (threadIdx.x >> 6);
-    if (n >= N) return;
-    const int nblk = (M + BM - 1) / BM;
-    const float* p0 = ws + part_idx(0, n, 0, N, M);
-    const float* p1 = ws + part_idx(1, n, 0, N, M);
-    double a = 0.0, b = 0.0, c = 0.0;
-    for (int k = lane; k < nblk; k += 64) {
-        a += (double)p0[k];
-        b += (double)p1[k];
-        c += (double)min(BM, M - k * BM) * blk_weight(gw, grows, k);
-    }
-    const double db = wave_sum_d(a), dg = wave_sum_d(b), Mw = wave_sum_d(c);
-    if (lane == 0) {
-        if (dbeta) dbeta[n] = accumulate ? dbeta[n] + (float)db : (float)db;
-        if (dgamma) dgamma[n] = accumulate ? dgamma[n] + (float)dg : (float)dg;
-        const double is = invstd[n];
-        const double k = (gamma ? (double)gamma[n] : 1.0) * is;
-        ca[n] = (float)k;
-        cb[n] = (float)(-k * is * dg / Mw);
-        cc[n] = (float)(-k * db / Mw);
-    }
-}
-
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ G, const float* __restrict__ Y,
         int M, int N, int ld, int res, const float* __restrict__ mean, const float* __restrict__ ca,
         const float* __restrict__ cb, const float* __restrict__ cc, float* __restrict__ dY, float* __restrict__ colsum,
@@ -2033,14 +1946,9 @@ int ured_bn_fwd_finalize(const float* stat_ws, int M, int N, const float* gamma,
     URED_REQUIRE(stat_ws && mean && invstd && scale && shift, "ured_bn_fwd_finalize: null pointer");
     URED_REQUIRE(!group_w || (group_rows > 0 && group_rows % BM == 0),
                  "ured_bn_fwd_finalize: row weights need group_rows multiple of %d (got %d)", BM, group_rows);
-    if (URED_BN_FIN_WAVE)
-        hipLaunchKernelGGL(bn_fwd_finalize_wave_kernel, dim3((N + BNF_WAVES - 1) / BNF_WAVES), dim3(64 * BNF_WAVES), 0,
-                           (hipStream_t)stream, stat_ws, M, N, gamma, beta, eps, momentum, running_mean, running_var,
-                           mean, invstd, scale, shift, group_w, group_rows, num_batches_tracked);
-    else
-        hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, stat_ws, M, N, gamma, beta,
-                           eps, momentum, running_mean, running_var, mean, invstd, scale, shift, group_w, group_rows,
-                           num_batches_tracked);
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, stat_ws, M, N, gamma, beta,
+                       eps, momentum, running_mean, running_var, mean, invstd, scale, shift, group_w, group_rows,
+                       num_batches_tracked);
     return ured::launch_status("ured_bn_fwd_finalize");
 }
 
@@ -2054,13 +1962,8 @@ int ured_bn_bwd_finalize(const float* bwd_ws, int M, int N, const float* gamma, 
     URED_REQUIRE(bwd_ws && invstd && coef_a && coef_b && coef_c, "ured_bn_bwd_finalize: null pointer");
     URED_REQUIRE(!group_w || (group_rows > 0 && group_rows % BM == 0),
                  "ured_bn_bwd_finalize: row weights need group_rows multiple of %d (got %d)", BM, group_rows);
-    if (URED_BN_FIN_WAVE)
-        hipLaunchKernelGGL(bn_bwd_finalize_wave_kernel, dim3((N + BNF_WAVES - 1) / BNF_WAVES), dim3(64 * BNF_WAVES), 0,
-                           (hipStream_t)stream, bwd_ws, M, N, gamma, invstd, dgamma, dbeta, accumulate, coef_a, coef_b,
-                           coef_c, group_w, group_rows);
-    else
-        hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, bwd_ws, M, N, gamma, invstd,
-                           dgamma, dbeta, accumulate, coef_a, coef_b, coef_c, group_w, group_rows);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, bwd_ws, M, N, gamma, invstd,
+                       dgamma, dbeta, accumulate, coef_a, coef_b, coef_c, group_w, group_rows);
     return ured::launch_status("ured_bn_bwd_finalize");
 }
 
