@@ -23,9 +23,14 @@ if "seq" in sys.argv:
     orig = node.launch
     node.launch = lambda *ds: [orig(d) for d in ds]
 if "noproj" in sys.argv:    # each projection group as its own launch
-    agn.node_proj = lambda xs, ws, bs, sh=None: tuple(node.node_proj((x,), [w], [b], (s,)) for x, w, b, s in
-                                                      zip(xs, ws, bs, sh or (None,) * len(xs))) \
-        if len(xs) > 1 else node.node_proj(xs, ws, bs, sh)
+    def _split_proj(xs, ws, bs, aliases=None):
+        al = tuple(aliases) if aliases is not None else (False,) * len(xs)
+        if len(xs) == 1:
+            return node.node_proj(xs, ws, bs, aliases=al)
+        outs = [node.node_proj((x,), [w], [b], aliases=(a,)) for x, w, b, a in zip(xs, ws, bs, al)]
+        ys = [o[0] if a else o for o, a in zip(outs, al)]
+        return tuple(ys) + tuple(o[1] for o, a in zip(outs, al) if a)
+    agn.node_proj = _split_proj
 if "noffn" in sys.argv:
     agn.ResidualAttentionMessagePropagation._node_ffn_ok = lambda self: False
 if "nopd" in sys.argv:
